@@ -1,0 +1,286 @@
+/*
+ * massrt.h — C ABI of the MI355X (gfx950) path-tracing hot path.
+ *
+ * Drop-in boundary for the reference's per-pixel-per-sample render loop:
+ *   fn render(image, event_proxy, world: World<B>, camera: Camera, frame_limit)
+ *   (/root/reference/src/main.rs:150-295)
+ * Everything the reference does below that call — Camera::ray
+ * (world.rs:53-63), Camera::trace (world.rs:65-79), World::intersect
+ * (world.rs:131-144), BvhNode/BoundingBox/Sphere/Triangle/Instance/Model
+ * intersect (geom.rs:56-425,503-593), Material scatter/emit
+ * (material.rs:192-329,385-389), Background (material.rs:39-89), Surface
+ * (texture.rs:117-194,277-299) and the per-pass ImageBuffer::set /
+ * Image::merge accumulation (main.rs:253-265,577-596,629-638) — runs on the
+ * GPU behind these entry points.
+ *
+ * Rules of the ABI:
+ *  - every function returns an int status: MRT_OK (0) or an MRT_ERR_* code;
+ *    the message is in mrt_last_error(ctx) (or mrt_global_last_error() for
+ *    calls without a context). No C++ exception or panic crosses the ABI.
+ *  - handles are opaque; calls on one context must be serialized by the caller.
+ *  - plain C types only (pointers + sizes). Host buffers are caller-owned.
+ *    Device memory for the scene is owned by the context.
+ *  - one context drives one GPU; multi-GPU = one process (rank) per GPU, each
+ *    rendering its shard of framebuffer tiles (mrt_render_args.shard_*).
+ *
+ * The reference's Rust side would bind these with `extern "C"` (see
+ * INTEGRATION.md); the C++ host in this repo (mass-raytrace_amd/csrc/host)
+ * mirrors the reference's Scene/World/Camera/Intersect/Material surface and
+ * produces mrt_scene_desc through the mrt_builder_* entry points below.
+ */
+#ifndef MASSRT_H
+#define MASSRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MRT_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define MRT_OK 0
+#define MRT_ERR_INVALID 1  /* bad argument / malformed scene */
+#define MRT_ERR_HIP 2      /* HIP runtime failure (no GPU, kernel fault...) */
+#define MRT_ERR_IO 3       /* loader could not read/parse a file */
+#define MRT_ERR_STATE 4    /* call out of order (e.g. render before upload) */
+#define MRT_ERR_NOMEM 5
+
+/* ---- child references of the boundary BVH ------------------------------
+ * A BvhNode child (geom.rs:103-107: Option<Box<dyn Intersect>>) is encoded as
+ * kind<<28 | index. MRT_REF_NONE is the `None` right child of a 1-item node
+ * (geom.rs:120-121). */
+#define MRT_REF_KIND_SHIFT 28u
+#define MRT_REF_INDEX_MASK 0x0FFFFFFFu
+#define MRT_REF_NONE 0u
+#define MRT_REF_NODE 1u     /* BvhNode            geom.rs:185-205 */
+#define MRT_REF_SPHERE 2u   /* Sphere             geom.rs:56-101  */
+#define MRT_REF_TRIANGLE 3u /* Triangle           geom.rs:503-593 */
+#define MRT_REF_INSTANCE 4u /* Instance (of BLAS) geom.rs:403-425 */
+#define MRT_REF_MODEL 5u    /* Model (owns BLAS)  geom.rs:317-333 */
+#define MRT_REF(kind, idx) ((((uint32_t)(kind)) << MRT_REF_KIND_SHIFT) | ((uint32_t)(idx)&MRT_REF_INDEX_MASK))
+#define MRT_REF_KIND(r) (((uint32_t)(r)) >> MRT_REF_KIND_SHIFT)
+#define MRT_REF_INDEX(r) (((uint32_t)(r)) & MRT_REF_INDEX_MASK)
+#define MRT_NO_MATERIAL 0xFFFFFFFFu
+
+/* ---- flat scene description (the reference tree, not our GPU layout) --- */
+typedef struct {
+  float min[3], max[3]; /* BoundingBox   geom.rs:207-211 */
+  uint32_t left, right; /* MRT_REF(...)  geom.rs:104-105 */
+} mrt_node;
+
+typedef struct {
+  float center[3];
+  float radius; /* negative radius flips normals (geom.rs:78) */
+  uint32_t material;
+} mrt_sphere;
+
+#define MRT_TRI_HAS_UV 1u /* Triangle::uvs is Some (with_norms_and_uvs) */
+typedef struct {
+  float a[3], b[3], c[3];                  /* vertex_a/b/c     geom.rs:436-438 */
+  float na[3], nb[3], nc[3];               /* normal_a/b/c     geom.rs:441-443 */
+  float uva[2], uvb[2], uvc[2];            /* UV               geom.rs:428-432 */
+  float tangent[3], bitangent[3];          /* geom.rs:444-445 */
+  uint32_t material;                       /* per-triangle material */
+  uint32_t flags;                          /* MRT_TRI_HAS_UV */
+} mrt_triangle;
+
+typedef struct {
+  float fwd[16];      /* column-major M4 (generic.rs:71-77): transform     */
+  float inv[16];      /*                                   inv_transform   */
+  uint32_t blas_root; /* MRT_REF_NODE index of the shared Arc<BvhNode>      */
+  uint32_t material;  /* override (with_material) or MRT_NO_MATERIAL        */
+} mrt_instance;
+
+typedef struct {
+  uint32_t blas_root; /* MRT_REF_NODE index */
+  uint32_t material;  /* Model::with_material override or MRT_NO_MATERIAL */
+} mrt_model;
+
+#define MRT_MAT_NONE 0u          /* impl Material for ()  material.rs:385-389 */
+#define MRT_MAT_LAMBERTIAN 1u    /* material.rs:192-225 */
+#define MRT_MAT_METAL 2u         /* material.rs:248-284 (param = fuzz, clamped) */
+#define MRT_MAT_DIELECTRIC 3u    /* material.rs:286-329 (param = refraction index) */
+#define MRT_MAT_DIFFUSE_LIGHT 4u /* material.rs:227-246 (emit) */
+typedef struct {
+  uint32_t kind;
+  uint32_t surface; /* index into surfaces (Lambertian/Metal) */
+  float param;
+  float emit[3];
+} mrt_material;
+
+#define MRT_SURF_SOLID 0u   /* SolidColor  texture.rs:179-194 */
+#define MRT_SURF_TEXTURE 1u /* Texture     texture.rs:117-149 */
+typedef struct {
+  uint32_t kind;
+  uint32_t texture;
+  float color[4];
+} mrt_surface;
+
+#define MRT_WRAP_MIRROR 0u /* unimplemented in the reference (texture.rs:280-282) */
+#define MRT_WRAP_REPEAT 1u
+#define MRT_WRAP_CLAMP 2u
+typedef struct {
+  uint32_t width, height, wrap;
+  const uint8_t* rgba; /* width*height*4 bytes, row 0 first (texture.rs:113) */
+} mrt_texture;
+
+#define MRT_BG_SOLID 0u     /* SolidBackground material.rs:39-53 */
+#define MRT_BG_SKY 1u       /* SkyBackground   material.rs:55-63 */
+#define MRT_BG_SKYSPHERE 2u /* SkySphere       material.rs:65-89 */
+typedef struct {
+  uint32_t kind;
+  uint32_t surface;
+  float color[3];
+} mrt_background;
+
+typedef struct {
+  const mrt_node* nodes;
+  uint32_t n_nodes;
+  const uint32_t* roots; /* World::objects in order (world.rs:97,131-144) */
+  uint32_t n_roots;
+  const mrt_sphere* spheres;
+  uint32_t n_spheres;
+  const mrt_triangle* triangles;
+  uint32_t n_triangles;
+  const mrt_instance* instances;
+  uint32_t n_instances;
+  const mrt_model* models;
+  uint32_t n_models;
+  const mrt_material* materials;
+  uint32_t n_materials;
+  const mrt_surface* surfaces;
+  uint32_t n_surfaces;
+  const mrt_texture* textures;
+  uint32_t n_textures;
+  mrt_background background;
+} mrt_scene_desc;
+
+/* Camera fields precomputed by Camera::new (world.rs:5-51). */
+typedef struct {
+  float origin[3];
+  float lower_left_corner[3];
+  float horizontal[3];
+  float vertical[3];
+  float u[3];
+  float v[3];
+  float lens_radius;
+} mrt_camera;
+
+/* One render call = samples [spp_begin, spp_begin+spp_count) of every pixel
+ * in this shard, ADDED in sample order into the accumulation buffers:
+ *   accum_rgb[3*p+c] += color_c, accum_bounces[p] += MAX_DEPTH-depth
+ * with p = y*width + x and y = 0 the BOTTOM row (main.rs:258-263,592-595,
+ * 629-638). Per-(pixel,sample) RNG: xoroshiro128** seeded by splitmix64 of
+ * (seed, p, sample) — results do not depend on the shard split. */
+#define MRT_TILE 8u /* framebuffer tiles are MRT_TILE x MRT_TILE pixels */
+typedef struct {
+  uint32_t width, height;
+  uint32_t spp_begin, spp_count;
+  uint64_t seed;
+  uint32_t max_depth;   /* MAX_DEPTH = 50 in the reference (main.rs:37) */
+  uint32_t shard_index; /* tiles t with t % shard_count == shard_index */
+  uint32_t shard_count; /* 0 or 1 = whole frame */
+  uint32_t flags;       /* MRT_RENDER_* */
+} mrt_render_args;
+#define MRT_RENDER_COUNTERS 1u /* collect traversal counters (slower) */
+
+/* Closest hit of one ray (parity entry point). */
+typedef struct {
+  uint32_t prim;      /* MRT_REF(kind, index) of the primitive hit, or NONE */
+  uint32_t container; /* MRT_REF(INSTANCE|MODEL, index) or NONE */
+  float t;
+  uint32_t front_face;
+} mrt_hit;
+
+/* Algorithmic work counters (SURVEY §8d bytes model). */
+typedef struct {
+  uint64_t samples;
+  uint64_t segments;        /* World::intersect calls */
+  uint64_t node_visits;     /* BoundingBox::hit calls */
+  uint64_t sphere_tests;
+  uint64_t triangle_tests;
+  uint64_t instance_entries;
+  uint64_t model_entries;
+  uint64_t closest_hits;
+  uint64_t texel_taps;
+  uint64_t bounces;
+} mrt_counters;
+
+typedef struct mrt_ctx mrt_ctx;
+
+/* ---- device context ---------------------------------------------------- */
+int mrt_create(int device, mrt_ctx** out);
+int mrt_destroy(mrt_ctx* ctx);
+const char* mrt_last_error(const mrt_ctx* ctx);
+const char* mrt_global_last_error(void);
+int mrt_abi_version(void);
+
+int mrt_upload_scene(mrt_ctx* ctx, const mrt_scene_desc* scene);
+int mrt_set_camera(mrt_ctx* ctx, const mrt_camera* camera);
+/* host buffers: accum_rgb = width*height*3 floats, accum_bounces = width*height */
+int mrt_render(mrt_ctx* ctx, const mrt_render_args* args, float* accum_rgb, uint32_t* accum_bounces);
+/* device buffers, enqueued on `hip_stream` (hipStream_t, may be NULL) */
+int mrt_render_device(mrt_ctx* ctx, const mrt_render_args* args, float* d_accum_rgb,
+                      uint32_t* d_accum_bounces, void* hip_stream);
+/* rays: n x {ox,oy,oz,dx,dy,dz} host floats; out: n hits */
+int mrt_trace_rays(mrt_ctx* ctx, const float* rays, uint32_t n, float t_min, float t_max, mrt_hit* out);
+int mrt_get_counters(mrt_ctx* ctx, mrt_counters* out);
+int mrt_reset_counters(mrt_ctx* ctx);
+/* bytes of device memory held for the scene */
+int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
+
+/* ---- host scene builder (C++ mirror of the reference trait surface) -----
+ * A builder owns a World under construction plus the scene RNG (fastrand
+ * wyrand restatement, seeded like main.rs:86). Model construction and
+ * build_bvh draw from it exactly where the reference does (geom.rs:111).
+ * Calls returning an index return >= 0 on success and -MRT_ERR_* on error;
+ * status calls return MRT_OK or a positive MRT_ERR_*. Message:
+ * mrt_builder_last_error() (thread-local). */
+typedef struct mrt_builder mrt_builder;
+int mrt_builder_new(uint64_t rng_seed, mrt_builder** out);
+int mrt_builder_free(mrt_builder* b);
+const char* mrt_builder_last_error(void);
+/* Scene::generate of a built-in scene, then World::build_bvh (main.rs:107-112).
+ * names: "sphere_grid", "cornell", "cube_field", "mesh_ply", "mesh_obj",
+ *        "mesh_obj_textured"; asset_dir holds cube.ply and generated assets. */
+int mrt_builder_builtin(mrt_builder* b, const char* name, float aspect_ratio, const char* asset_dir);
+float mrt_builder_rand_f32(mrt_builder* b); /* f32::rand() on the scene stream */
+/* surfaces / materials; each returns an index >= 0 */
+int mrt_builder_solid(mrt_builder* b, float r, float g, float bl, float a);
+int mrt_builder_texture_png(mrt_builder* b, const char* path, uint32_t wrap);
+int mrt_builder_texture_rgba(mrt_builder* b, const uint8_t* rgba, uint32_t w, uint32_t h, uint32_t wrap);
+int mrt_builder_material(mrt_builder* b, uint32_t kind, uint32_t surface, float param, float er, float eg, float eb);
+int mrt_builder_background(mrt_builder* b, uint32_t kind, uint32_t surface, float r, float g, float bl);
+/* world objects (World::add, world.rs:112-115) */
+int mrt_builder_add_sphere(mrt_builder* b, uint32_t material, float cx, float cy, float cz, float radius);
+int mrt_builder_add_triangle(mrt_builder* b, uint32_t material, const float* abc /*9*/);
+/* Model::new / with_material over a triangle list (geom.rs:280-310); draws
+ * the BLAS BVH immediately. tris: n x 9 floats (Triangle::new) or, when
+ * shading != NULL, n x 24 floats {v,n,uv} x3 (Triangle::with_norms_and_uvs).
+ * Returns model handle index. add_to_world: also World::add(model). */
+int mrt_builder_model(mrt_builder* b, uint32_t tri_material, uint32_t override_material, const float* tris,
+                      uint32_t n, int with_shading, int add_to_world);
+int mrt_builder_model_from_ply(mrt_builder* b, const char* path, uint32_t tri_material,
+                               uint32_t override_material, int add_to_world);
+int mrt_builder_add_instance(mrt_builder* b, int model, const float* translation, const float* rotation,
+                             const float* scale, uint32_t material);
+int mrt_builder_camera(mrt_builder* b, float vfov, const float* look_from, const float* look_at,
+                       const float* view_up, float aspect, float aperture, float focus_distance);
+int mrt_builder_build_bvh(mrt_builder* b); /* World::build_bvh (world.rs:117-122) */
+/* flatten; pointers stay valid until the builder is freed or modified */
+int mrt_builder_desc(mrt_builder* b, mrt_scene_desc* desc, mrt_camera* camera);
+
+/* ---- loaders (host; ply_loader.rs, obj_loader.rs, stl_loader.rs) -------- */
+/* returns triangle count (or -MRT_ERR_IO); out (if non-NULL, capacity cap triangles) gets 9 floats per tri */
+int64_t mrt_load_ply(const char* path, float* out, uint64_t cap);
+int64_t mrt_load_stl(const char* path, float* out, uint64_t cap);
+/* OBJ with v/vt/vn: 24 floats per tri {v(3),n(3),uv(2)} x3, uv as read (obj_fns) */
+int64_t mrt_load_obj(const char* path, float* out, uint64_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MASSRT_H */

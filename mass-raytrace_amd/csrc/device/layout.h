@@ -1,0 +1,71 @@
+// layout.h — the scene as it lives in HBM (built by upload.cpp from an
+// mrt_scene_desc, read by the gfx950 kernels).
+//
+// The reference traverses a binary BvhNode tree recursively, LEFT child first,
+// shrinking t_max as hits are found (geom.rs:185-205), and World::intersect
+// walks its object list in order (world.rs:131-144). That visiting order is
+// fixed (it does not depend on the ray), so the tree is linearised here in
+// that exact depth-first preorder with a skip index per box ("threaded BVH"):
+//   box hit  -> next record (first child)      box miss -> skip (past subtree)
+//   primitive -> next record
+// This reproduces the reference's sequence of box and primitive tests — and
+// therefore its closest hit, ties included — with no traversal stack.
+// Instances/models jump into a shared BLAS region and return (one level).
+//
+// Records are made of 16-byte slots (uint4); the kind is always slot1.w:
+//   BOX    2 slots  {min.x,min.y,min.z,max.x} {max.y,max.z,skip,BOX}
+//   SPHERE 2 slots  {cx,cy,cz,r}              {sphere_id,0,0,SPHERE}
+//   TRI    3 slots  {a.x,a.y,a.z,ab.x}        {ab.y,ab.z,tri_id,TRI} {ac.x,ac.y,ac.z,flags}
+//   INST   2 slots  {inst_id,blas_begin,blas_end,0} {0,0,0,INST}
+//   MODEL  2 slots  {model_id,blas_begin,blas_end,0} {0,0,0,MODEL}
+// ab = b - a and ac = c - a are precomputed on the host with the same IEEE
+// subtraction Triangle::intersect performs (geom.rs:505-506).
+#pragma once
+#include <stdint.h>
+
+namespace mrt {
+
+enum : uint32_t { KIND_BOX = 1, KIND_SPHERE = 2, KIND_TRI = 3, KIND_INST = 4, KIND_MODEL = 5 };
+enum : uint32_t { TRI_FLAG_ALPHA = 1u, TRI_FLAG_UV = 2u };
+
+// Flattened material: surface resolved in place.
+//   q0 = {kind, surf_kind, texture, param bits}
+//   q1 = {color/emit rgba as float bits}
+struct GpuMaterial {
+  uint32_t kind, surf_kind, texture;
+  float param;
+  float color[4];  // SolidColor rgba (Lambertian/Metal) or emit rgb (DiffuseLight)
+};
+
+struct GpuTexture {
+  uint32_t width, height, wrap;
+  uint32_t offset;  // first texel in the texel array
+};
+
+// Per-triangle shading record, 7 x float4 (112 B):
+//  0 {a.x a.y a.z b.x} 1 {b.y b.z c.x c.y} 2 {c.z na.x na.y na.z}
+//  3 {nb.x nb.y nb.z nc.x} 4 {nc.y nc.z uva.x uva.y} 5 {uvb.x uvb.y uvc.x uvc.y}
+//  6 {material, flags, 0, 0}
+constexpr uint32_t kTriShadeQuads = 7;
+
+// Kernel-visible scene (plain pointers into one device allocation).
+struct DevScene {
+  const uint32_t* slots;  // n_slots * 4 words
+  uint32_t world_begin, world_end;
+  const float* inst_inv;   // 12 floats per instance: c0.xyz c1.xyz c2.xyz c3.xyz
+  const float* inst_fwd;   // 12 floats per instance
+  const uint32_t* inst_mat;  // override material or 0xFFFFFFFF
+  const uint32_t* model_mat;
+  const float* sph;        // 4 floats per sphere: cx cy cz r
+  const uint32_t* sph_mat;
+  const float* tri_shade;  // kTriShadeQuads*4 floats per triangle
+  const GpuMaterial* materials;
+  const GpuTexture* textures;
+  const uint32_t* texels;  // RGBA8 packed little-endian
+  uint32_t bg_kind;
+  uint32_t bg_texture;  // SkySphere texture (surface must be a texture or solid)
+  uint32_t bg_surf_kind;
+  float bg_color[4];
+};
+
+}  // namespace mrt

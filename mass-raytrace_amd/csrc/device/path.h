@@ -1,0 +1,434 @@
+// path.h — device-side restatement of the reference hot path for gfx950.
+//   BoundingBox::hit      geom.rs:218-247
+//   Sphere::intersect     geom.rs:56-93
+//   Triangle::intersect   geom.rs:504-585 (candidate test; shading deferred)
+//   Instance::intersect   geom.rs:403-420
+//   BvhNode::intersect    geom.rs:185-205 (via the preorder stream, layout.h)
+//   World::intersect      world.rs:131-144
+//   Camera::ray           world.rs:53-63
+//   Material::scatter/emit material.rs:203-329,385-389
+//   Background            material.rs:49-89
+//   Texture::get_f        texture.rs:126-148, WrapMode::wrap texture.rs:278-299
+// All arithmetic follows mrt_math.h's evaluation order; build with
+// -ffp-contract=off and correctly rounded f32 divide/sqrt.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../mrt_math.h"
+#include "../mrt_rng.h"
+#include "layout.h"
+
+namespace mrt {
+
+#define MRT_DEV __device__ __forceinline__
+
+constexpr uint32_t kRefNone = 0u;
+MRT_DEV uint32_t make_ref(uint32_t kind, uint32_t idx) { return (kind << 28) | idx; }
+
+struct DevCounters {
+  unsigned long long samples, segments, node_visits, sphere_tests, triangle_tests, instance_entries,
+      model_entries, closest_hits, texel_taps, bounces;
+};
+
+struct LocalCounters {
+  uint32_t node_visits = 0, sphere_tests = 0, triangle_tests = 0, instance_entries = 0, model_entries = 0,
+           texel_taps = 0;
+};
+
+MRT_DEV float u2f(uint32_t u) { return __uint_as_float(u); }
+MRT_DEV V3 ld3(const float* p) { return V3{p[0], p[1], p[2]}; }
+
+// ---- textures -----------------------------------------------------------
+MRT_DEV float rust_fract(float x) { return x - truncf(x); }
+// `f32 as usize` saturates: NaN and negatives -> 0
+MRT_DEV uint32_t f2usize(float f) { return f > 0.0f ? (f < 4294967040.0f ? (uint32_t)f : 0xFFFFFFFFu) : 0u; }
+
+MRT_DEV V4 texel(const DevScene& S, const GpuTexture& t, uint32_t x, uint32_t y) {
+  uint32_t v = S.texels[t.offset + y * t.width + x];
+  return V4{(float)(v & 255u) / 255.0f, (float)((v >> 8) & 255u) / 255.0f, (float)((v >> 16) & 255u) / 255.0f,
+            (float)(v >> 24) / 255.0f};
+}
+
+MRT_DEV V4 texture_get_f(const DevScene& S, uint32_t tex, V2 uv, LocalCounters& lc) {
+  const GpuTexture t = S.textures[tex];
+  float x = uv.x, y = uv.y;
+  if (t.wrap == MRT_WRAP_REPEAT) {
+    x = x < 0.0f ? 1.0f - rust_fract(fabsf(x)) : x;
+    y = y < 0.0f ? 1.0f - rust_fract(fabsf(y)) : y;
+    x = x > 1.0f ? rust_fract(x) : x;
+    y = y > 1.0f ? rust_fract(y) : y;
+  } else {
+    x = fmaxf(fminf(x, 1.0f), 0.0f);
+    y = fmaxf(fminf(y, 1.0f), 0.0f);
+  }
+  x = x * (float)(t.width - 1);
+  y = y * (float)(t.height - 1);
+  uint32_t x0 = f2usize(floorf(x)), x1 = f2usize(ceilf(x));
+  uint32_t y0 = f2usize(floorf(y)), y1 = f2usize(ceilf(y));
+  x0 = x0 < t.width ? x0 : t.width - 1;  // the reference would panic out of range
+  x1 = x1 < t.width ? x1 : t.width - 1;
+  y0 = y0 < t.height ? y0 : t.height - 1;
+  y1 = y1 < t.height ? y1 : t.height - 1;
+  float tt = x - (float)x0;
+  V4 p0 = texel(S, t, x0, y0) * (1.0f - tt) + texel(S, t, x1, y0) * tt;
+  V4 p1 = texel(S, t, x0, y1) * (1.0f - tt) + texel(S, t, x1, y1) * tt;
+  tt = y - (float)y0;
+  lc.texel_taps += 4;
+  return p1 * tt + p0 * (1.0f - tt);
+}
+
+MRT_DEV V4 surface_get_f(const DevScene& S, const GpuMaterial& m, V2 uv, LocalCounters& lc) {
+  if (m.surf_kind == MRT_SURF_TEXTURE) return texture_get_f(S, m.texture, uv, lc);
+  return V4{m.color[0], m.color[1], m.color[2], m.color[3]};
+}
+
+// ---- primitive tests -------------------------------------------------------
+// BoundingBox::hit: 6 true divisions; the per-axis early-outs cannot change the
+// result (t0 only grows, t1 only shrinks), so one final compare is equivalent.
+MRT_DEV bool box_hit(V3 mn, V3 mx, V3 o, V3 d, float tmin, float tmax) {
+  V3 a = (mn - o) / d;
+  V3 b = (mx - o) / d;
+  V3 lo = vmin(a, b), hi = vmax(a, b);
+  float t0 = fmaxf(lo.x, tmin), t1 = fminf(hi.x, tmax);
+  t0 = fmaxf(lo.y, t0), t1 = fminf(hi.y, t1);
+  t0 = fmaxf(lo.z, t0), t1 = fminf(hi.z, t1);
+  return !(t1 < t0);
+}
+
+MRT_DEV bool sphere_hit(V3 c, float r, V3 o, V3 d, float tmin, float tmax, float& t) {
+  V3 oc = o - c;
+  float a = length_squared(d);
+  float half_b = dot(oc, d);
+  float cc = length_squared(oc) - (r * r);
+  float disc = (half_b * half_b) - (a * cc);
+  if (disc < 0.0f) return false;
+  float sq = sqrtf(disc);
+  float root = (-half_b - sq) / a;
+  if (root < tmin || tmax < root) {
+    root = (-half_b + sq) / a;
+    if (root < tmin || tmax < root) return false;
+  }
+  t = root;
+  return true;
+}
+
+MRT_DEV bool tri_hit(V3 a, V3 ab, V3 ac, V3 o, V3 d, float tmin, float tmax, float& t) {
+  V3 p_vec = cross(d, ac);
+  float det = dot(ab, p_vec);
+  if (fabsf(det) < 0.000001f) return false;
+  float inv_det = 1.0f / det;
+  V3 t_vec = o - a;
+  float u = dot(t_vec, p_vec) * inv_det;
+  if (u < 0.0f || u > 1.0f) return false;
+  V3 q_vec = cross(t_vec, ab);
+  float v = dot(d, q_vec) * inv_det;
+  if (v < 0.0f || v + u > 1.0f) return false;
+  float tt = dot(ac, q_vec) * inv_det;
+  if (tt < tmin || tt > tmax) return false;
+  t = tt;
+  return true;
+}
+
+struct TriShade {
+  V3 a, b, c, na, nb, nc;
+  V2 uva, uvb, uvc;
+  uint32_t material, flags;
+};
+MRT_DEV TriShade load_tri(const DevScene& S, uint32_t id) {
+  const float4* q = reinterpret_cast<const float4*>(S.tri_shade) + (size_t)id * kTriShadeQuads;
+  float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4], q5 = q[5], q6 = q[6];
+  TriShade s;
+  s.a = V3{q0.x, q0.y, q0.z};
+  s.b = V3{q0.w, q1.x, q1.y};
+  s.c = V3{q1.z, q1.w, q2.x};
+  s.na = V3{q2.y, q2.z, q2.w};
+  s.nb = V3{q3.x, q3.y, q3.z};
+  s.nc = V3{q3.w, q4.x, q4.y};
+  s.uva = V2{q4.z, q4.w};
+  s.uvb = V2{q5.x, q5.y};
+  s.uvc = V2{q5.z, q5.w};
+  s.material = __float_as_uint(q6.x);
+  s.flags = __float_as_uint(q6.y);
+  return s;
+}
+
+// Area-ratio barycentrics of the accepted point (geom.rs:535-547)
+MRT_DEV void tri_bary(const TriShade& s, V3 point, float& a0, float& a1, float& a2) {
+  V3 d0 = s.a - point, d1 = s.b - point, d2 = s.c - point;
+  float area = length(cross(s.a - s.b, s.a - s.c));
+  a0 = length(cross(d1, d2)) / area;
+  a1 = length(cross(d2, d0)) / area;
+  a2 = length(cross(d0, d1)) / area;
+}
+
+// Material::alpha_test of the triangle's OWN material (geom.rs:567-571,
+// material.rs:222-224,281-283): surface alpha != 0.
+MRT_DEV bool tri_alpha_pass(const DevScene& S, uint32_t id, V3 o, V3 d, float t, LocalCounters& lc) {
+  TriShade s = load_tri(S, id);
+  V3 point = o + d * t;
+  float a0, a1, a2;
+  tri_bary(s, point, a0, a1, a2);
+  V2 uv = (s.uva * a0 + s.uvb * a1) + s.uvc * a2;
+  const GpuMaterial m = S.materials[s.material];
+  if (m.kind != MRT_MAT_LAMBERTIAN && m.kind != MRT_MAT_METAL) return true;
+  return surface_get_f(S, m, uv, lc).w != 0.0f;
+}
+
+MRT_DEV void load_m12(const float* p, V3& c0, V3& c1, V3& c2, V3& c3) {
+  c0 = V3{p[0], p[1], p[2]};
+  c1 = V3{p[3], p[4], p[5]};
+  c2 = V3{p[6], p[7], p[8]};
+  c3 = V3{p[9], p[10], p[11]};
+}
+// M4::transform (generic.rs:106-115) on the xyz rows: ((c0*x + c1*y) + c2*z) + c3*w
+MRT_DEV V3 xform(V3 c0, V3 c1, V3 c2, V3 c3, V3 p, float w) {
+  return ((c0 * p.x + c1 * p.y) + c2 * p.z) + c3 * w;
+}
+
+struct Hit {
+  float t;
+  uint32_t prim;       // make_ref(kind, id) or kRefNone
+  uint32_t container;  // make_ref(INSTANCE|MODEL, id) or kRefNone
+};
+
+// World::intersect(ray, t_min, t_max) over the preorder stream.
+template <bool COUNT>
+MRT_DEV Hit closest_hit(const DevScene& S, V3 o, V3 d, float tmin, float tmax, LocalCounters& lc) {
+  const uint4* slots = reinterpret_cast<const uint4*>(S.slots);
+  uint32_t i = S.world_begin, end = S.world_end, ret = 0;
+  bool in_blas = false;
+  V3 ro = o, rd = d;
+  uint32_t container = kRefNone;
+  Hit h{tmax, kRefNone, kRefNone};
+  float best = tmax;
+  for (;;) {
+    if (i >= end) {
+      if (!in_blas) break;
+      in_blas = false;
+      i = ret;
+      end = S.world_end;
+      ro = o;
+      rd = d;
+      container = kRefNone;
+      continue;
+    }
+    const uint4 s0 = slots[i];
+    const uint4 s1 = slots[i + 1];
+    const uint32_t kind = s1.w;
+    if (kind == KIND_BOX) {
+      if (COUNT) lc.node_visits++;
+      V3 mn{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, mx{u2f(s0.w), u2f(s1.x), u2f(s1.y)};
+      i = box_hit(mn, mx, ro, rd, tmin, best) ? i + 2 : s1.z;
+    } else if (kind == KIND_TRI) {
+      if (COUNT) lc.triangle_tests++;
+      const uint4 s2 = slots[i + 2];
+      V3 a{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, ab{u2f(s0.w), u2f(s1.x), u2f(s1.y)},
+          ac{u2f(s2.x), u2f(s2.y), u2f(s2.z)};
+      float t;
+      if (tri_hit(a, ab, ac, ro, rd, tmin, best, t)) {
+        if (!(s2.w & TRI_FLAG_ALPHA) || tri_alpha_pass(S, s1.z, ro, rd, t, lc)) {
+          best = t;
+          h.t = t;
+          h.prim = make_ref(MRT_REF_TRIANGLE, s1.z);
+          h.container = container;
+        }
+      }
+      i += 3;
+    } else if (kind == KIND_SPHERE) {
+      if (COUNT) lc.sphere_tests++;
+      float t;
+      if (sphere_hit(V3{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, u2f(s0.w), ro, rd, tmin, best, t)) {
+        best = t;
+        h.t = t;
+        h.prim = make_ref(MRT_REF_SPHERE, s1.x);
+        h.container = container;
+      }
+      i += 2;
+    } else if (kind == KIND_INST) {
+      if (COUNT) lc.instance_entries++;
+      V3 c0, c1, c2, c3;
+      load_m12(S.inst_inv + (size_t)s0.x * 12, c0, c1, c2, c3);
+      ro = xform(c0, c1, c2, c3, o, 1.0f);
+      rd = xform(c0, c1, c2, c3, d, 0.0f);
+      container = make_ref(MRT_REF_INSTANCE, s0.x);
+      ret = i + 2;
+      i = s0.y;
+      end = s0.z;
+      in_blas = true;
+    } else {  // KIND_MODEL
+      if (COUNT) lc.model_entries++;
+      container = make_ref(MRT_REF_MODEL, s0.x);
+      ret = i + 2;
+      i = s0.y;
+      end = s0.z;
+      in_blas = true;
+    }
+  }
+  return h;
+}
+
+// Hit record of the closest hit, computed the way the reference's winning
+// intersect computed it (geom.rs:77-91,535-584,405-419,318-326).
+struct Surf {
+  V3 point, normal;
+  V2 uv;
+  bool has_uv, front_face;
+  uint32_t material;
+};
+
+MRT_DEV Surf resolve_hit(const DevScene& S, V3 o, V3 d, const Hit& h) {
+  Surf s;
+  V3 ro = o, rd = d;
+  const uint32_t ckind = h.container >> 28, cidx = h.container & 0x0FFFFFFFu;
+  V3 f0, f1, f2, f3;
+  if (ckind == MRT_REF_INSTANCE) {
+    V3 c0, c1, c2, c3;
+    load_m12(S.inst_inv + (size_t)cidx * 12, c0, c1, c2, c3);
+    ro = xform(c0, c1, c2, c3, o, 1.0f);
+    rd = xform(c0, c1, c2, c3, d, 0.0f);
+  }
+  const uint32_t pkind = h.prim >> 28, pidx = h.prim & 0x0FFFFFFFu;
+  V3 outward;
+  s.point = ro + rd * h.t;
+  if (pkind == MRT_REF_SPHERE) {
+    V3 c = ld3(S.sph + (size_t)pidx * 4);
+    float r = S.sph[(size_t)pidx * 4 + 3];
+    outward = (s.point - c) / r;
+    s.has_uv = false;
+    s.uv = V2{0, 0};
+    s.material = S.sph_mat[pidx];
+  } else {
+    TriShade t = load_tri(S, pidx);
+    float a0, a1, a2;
+    tri_bary(t, s.point, a0, a1, a2);
+    outward = (t.na * a0 + t.nb * a1) + t.nc * a2;
+    s.has_uv = (t.flags & TRI_FLAG_UV) != 0;
+    s.uv = s.has_uv ? (t.uva * a0 + t.uvb * a1) + t.uvc * a2 : V2{0, 0};
+    s.material = t.material;
+  }
+  // Hit::set_face_normal in the intersecting (object) space (geom.rs:17-24)
+  s.front_face = dot(rd, outward) < 0.0f;
+  s.normal = s.front_face ? outward : -outward;
+  if (ckind == MRT_REF_INSTANCE) {
+    load_m12(S.inst_fwd + (size_t)cidx * 12, f0, f1, f2, f3);
+    s.point = xform(f0, f1, f2, f3, s.point, 1.0f);
+    s.normal = unit(xform(f0, f1, f2, f3, s.normal, 0.0f));
+    uint32_t m = S.inst_mat[cidx];
+    if (m != MRT_NO_MATERIAL) s.material = m;
+  } else if (ckind == MRT_REF_MODEL) {
+    uint32_t m = S.model_mat[cidx];
+    if (m != MRT_NO_MATERIAL) s.material = m;
+  }
+  return s;
+}
+
+// ---- sampling (math.rs:262-291) -----------------------------------------------
+MRT_DEV V3 random_in_unit_sphere(PathRng& rng) {
+  for (;;) {
+    float x = rng.f32() * 2.0f - 1.0f;
+    float y = rng.f32() * 2.0f - 1.0f;
+    float z = rng.f32() * 2.0f - 1.0f;
+    V3 v{x, y, z};
+    if (length_squared(v) >= 1.0f) continue;
+    return v;
+  }
+}
+MRT_DEV V3 random_in_unit_disk(PathRng& rng) {
+  for (;;) {
+    float x = rng.f32() * 2.0f - 1.0f;
+    float y = rng.f32() * 2.0f - 1.0f;
+    V3 v{x, y, 0.0f};
+    if (length_squared(v) >= 1.0f) continue;
+    return v;
+  }
+}
+
+// Dielectric::reflectance (material.rs:296-299); powi(5) = x*((x*x)*(x*x))
+MRT_DEV float reflectance(float cosine, float ref_idx) {
+  float r0 = (1.0f - ref_idx) / (1.0f + ref_idx);
+  r0 = r0 * r0;
+  float x = 1.0f - cosine;
+  return r0 + (1.0f - r0) * (x * ((x * x) * (x * x)));
+}
+
+struct DevCamera {
+  V3 origin, llc, horizontal, vertical, u, v;
+  float lens_radius;
+};
+
+// main.rs:258-260 + Camera::ray (world.rs:53-63)
+MRT_DEV void camera_ray(const DevCamera& cam, uint32_t x, uint32_t y, uint32_t W, uint32_t H, PathRng& rng, V3& o,
+                        V3& d) {
+  float u = ((float)x + rng.f32()) / (float)(W - 1);
+  float v = ((float)y + rng.f32()) / (float)(H - 1);
+  V3 blur = random_in_unit_disk(rng) * cam.lens_radius;
+  V3 offset = cam.u * blur.x + cam.v * blur.y;
+  o = cam.origin + offset;
+  d = (((cam.llc + (cam.horizontal * u)) + (cam.vertical * v)) - cam.origin) - offset;
+}
+
+MRT_DEV V3 background(const DevScene& S, V3 d, LocalCounters& lc) {
+  if (S.bg_kind == MRT_BG_SOLID) return V3{S.bg_color[0], S.bg_color[1], S.bg_color[2]};
+  if (S.bg_kind == MRT_BG_SKY) {
+    V3 ud = unit(d);
+    float t = 0.5f * (ud.y + 1.0f);
+    return (fill3(1.0f) * (1.0f - t)) + (V3{0.5f, 0.7f, 1.0f} * t);
+  }
+  V3 p = unit(d);
+  float theta = acosf(p.y);
+  float phi = atan2f(p.z * -1.0f, p.x) + kPi;
+  V2 uv{phi / (2.0f * kPi), theta / kPi};
+  V4 px = S.bg_surf_kind == MRT_SURF_TEXTURE ? texture_get_f(S, S.bg_texture, uv, lc)
+                                             : V4{S.bg_color[0], S.bg_color[1], S.bg_color[2], S.bg_color[3]};
+  return V3{px.x, px.y, px.z};
+}
+
+// Hit::emit + Hit::scatter (geom.rs:26-32). Returns true when the path
+// continues with (new_o, new_d) and attenuation `atten`.
+MRT_DEV bool scatter(const DevScene& S, const Surf& s, V3 d, PathRng& rng, V3& emitted, V3& atten, V3& new_d,
+                     LocalCounters& lc) {
+  const GpuMaterial m = S.materials[s.material];
+  emitted = V3{0, 0, 0};
+  V2 uv = s.has_uv ? s.uv : V2{0, 0};
+  switch (m.kind) {
+    case MRT_MAT_LAMBERTIAN: {
+      V3 dir = s.normal + unit(random_in_unit_sphere(rng));
+      if (near_zero(dir)) dir = s.normal;
+      V4 c = surface_get_f(S, m, uv, lc);
+      atten = V3{c.x, c.y, c.z};
+      new_d = dir;
+      return true;
+    }
+    case MRT_MAT_METAL: {
+      V3 reflected = reflect(unit(d), s.normal);
+      V3 dir = reflected + (random_in_unit_sphere(rng) * m.param);
+      if (dot(dir, s.normal) > 0.0f) {
+        V4 c = surface_get_f(S, m, uv, lc);
+        atten = V3{c.x, c.y, c.z};
+        new_d = dir;
+        return true;
+      }
+      return false;
+    }
+    case MRT_MAT_DIELECTRIC: {
+      float ratio = s.front_face ? 1.0f / m.param : m.param;
+      V3 ud = unit(d);
+      float cos_theta = fminf(dot(-ud, s.normal), 1.0f);
+      float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
+      bool cannot_refract = ratio * sin_theta > 1.0f;
+      if (cannot_refract || reflectance(cos_theta, ratio) > rng.f32())
+        new_d = reflect(ud, s.normal);
+      else
+        new_d = refract(ud, s.normal, ratio);
+      atten = fill3(1.0f);
+      return true;
+    }
+    case MRT_MAT_DIFFUSE_LIGHT:
+      emitted = V3{m.color[0], m.color[1], m.color[2]};
+      return false;
+    default:
+      return false;
+  }
+}
+
+}  // namespace mrt

@@ -1,0 +1,716 @@
+// render.hip — the wavefront path-tracing integrator for gfx950 and the
+// device half of the C ABI (include/massrt.h).
+//
+// Replaces render()'s per-thread pixel loop (main.rs:235-290): each sample
+// (one camera path, main.rs:257-263) becomes a path slot in a pool of SoA
+// HBM buffers, advanced one segment per iteration by two kernels:
+//   k_trace : closest hit of every active ray (World::intersect)      [k2]
+//   k_shade : emit/scatter/background, path termination, regeneration of
+//             finished slots with new camera rays (Camera::ray) and wave
+//             ballot/prefix-sum compaction of the survivors           [k1,k3,k4]
+// Finished samples are written to a per-(sample,pixel) result slab and folded
+// into the caller's accumulation buffers in sample order by k_accumulate [k5]
+// (Image::merge, main.rs:629-638), so the sums do not depend on scheduling
+// or on how tiles are sharded across GPUs.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../../include/massrt.h"
+#include "path.h"
+#include "upload.h"
+
+using namespace mrt;
+
+namespace {
+
+struct HipError {
+  std::string msg;
+};
+#define HIP_CHECK(x)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) throw HipError{std::string(#x) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+
+struct ApiError {
+  int code;
+  std::string msg;
+};
+
+constexpr int kBlock = 256;
+
+struct Ctrl {
+  uint32_t active[2];
+  uint32_t next_work;
+  uint32_t pad;
+};
+
+// SoA path state, 5 x 16 B per slot:
+//   ro  = {o.x, o.y, o.z, work index g}    rd  = {d.x, d.y, d.z, bounces k}
+//   thr = {T.x, T.y, T.z, -}               rad = {L.x, L.y, L.z, -}
+//   rng = xoroshiro128** {s0.lo, s0.hi, s1.lo, s1.hi}
+struct PathBufs {
+  float4* ro;
+  float4* rd;
+  float4* thr;
+  float4* rad;
+  uint4* rng;
+};
+
+struct RenderParams {
+  uint32_t W, H;
+  unsigned long long seed;
+  uint32_t max_depth;
+  uint32_t n_pix;        // pixels in this shard
+  uint32_t G;            // work items in this chunk = n_pix * samples
+  uint32_t sample_base;  // absolute sample index of chunk sample 0
+  const uint32_t* pixlist;
+};
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint32_t lane_rank(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ void flush_counters(DevCounters* c, const LocalCounters& lc, uint32_t segs, uint32_t hits,
+                               uint32_t samples, uint32_t bounces) {
+  uint32_t v[10] = {samples, segs, lc.node_visits, lc.sphere_tests, lc.triangle_tests, lc.instance_entries,
+                    lc.model_entries, hits, lc.texel_taps, bounces};
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(c);
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    uint32_t s = wave_sum(v[k]);
+    if (lane_id() == 0 && s) atomicAdd(dst + k, (unsigned long long)s);
+  }
+}
+
+__device__ __forceinline__ void gen_work(const DevCamera& cam, const RenderParams& rp, uint32_t g, float4& ro,
+                                         float4& rd, uint4& rs) {
+  uint32_t s_local = g / rp.n_pix;
+  uint32_t lp = g - s_local * rp.n_pix;
+  uint32_t p = rp.pixlist[lp];
+  uint32_t y = p / rp.W, x = p - y * rp.W;
+  PathRng rng = path_rng(rp.seed, p, rp.sample_base + s_local);
+  V3 o, d;
+  camera_ray(cam, x, y, rp.W, rp.H, rng, o, d);
+  ro = make_float4(o.x, o.y, o.z, __uint_as_float(g));
+  rd = make_float4(d.x, d.y, d.z, __uint_as_float(0u));
+  rs = make_uint4((uint32_t)rng.s0, (uint32_t)(rng.s0 >> 32), (uint32_t)rng.s1, (uint32_t)(rng.s1 >> 32));
+}
+
+__global__ __launch_bounds__(kBlock) void k_generate(DevCamera cam, RenderParams rp, PathBufs out, uint32_t n0) {
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n0) return;
+  float4 ro, rd;
+  uint4 rs;
+  gen_work(cam, rp, i, ro, rd, rs);
+  out.ro[i] = ro;
+  out.rd[i] = rd;
+  out.thr[i] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+  out.rad[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  out.rng[i] = rs;
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
+                                                  DevCounters* cnt) {
+  const uint32_t n = ctrl->active[cur];
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = 0;
+  const uint32_t base = blockIdx.x * kBlock;
+  if (base >= n) return;
+  const uint32_t i = base + threadIdx.x;
+  LocalCounters lc;
+  uint32_t seg = 0, nh = 0;
+  if (i < n) {
+    float4 o4 = in.ro[i], d4 = in.rd[i];
+    Hit h = closest_hit<COUNT>(S, V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, 0.001f, INFINITY, lc);
+    hits[i] = make_uint4(__float_as_uint(h.t), h.prim, h.container, 0u);
+    seg = 1;
+    nh = h.prim != kRefNone;
+  }
+  if (COUNT) flush_counters(cnt, lc, seg, nh, 0, 0);
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_shade(DevScene S, DevCamera cam, RenderParams rp, PathBufs in,
+                                                  PathBufs out, const uint4* hits, Ctrl* ctrl, uint32_t cur,
+                                                  float4* results, DevCounters* cnt) {
+  const uint32_t n = ctrl->active[cur];
+  const uint32_t base = blockIdx.x * kBlock;
+  if (base >= n) return;
+  const uint32_t i = base + threadIdx.x;
+  LocalCounters lc;
+  bool alive = false, need = false;
+  float4 ro{}, rd{}, thr{}, rad{};
+  uint4 rs{};
+  uint32_t nbounce = 0, nsample = 0;
+  if (i < n) {
+    ro = in.ro[i];
+    rd = in.rd[i];
+    thr = in.thr[i];
+    rad = in.rad[i];
+    rs = in.rng[i];
+    const uint4 hv = hits[i];
+    Hit h{__uint_as_float(hv.x), hv.y, hv.z};
+    V3 o{ro.x, ro.y, ro.z}, d{rd.x, rd.y, rd.z}, T{thr.x, thr.y, thr.z}, L{rad.x, rad.y, rad.z};
+    uint32_t g = __float_as_uint(ro.w), k = __float_as_uint(rd.w);
+    PathRng rng{(unsigned long long)rs.x | ((unsigned long long)rs.y << 32),
+                (unsigned long long)rs.z | ((unsigned long long)rs.w << 32)};
+    bool cont = false;
+    if (h.prim != kRefNone) {
+      Surf s = resolve_hit(S, o, d, h);
+      V3 emitted, atten, nd;
+      cont = scatter(S, s, d, rng, emitted, atten, nd, lc);
+      L = L + T * emitted;
+      if (cont) {
+        T = T * atten;
+        k += 1;
+        nbounce = 1;
+        o = s.point;
+        d = nd;
+        if (k >= rp.max_depth) cont = false;  // trace(depth 0) returns (0, 0)
+      }
+    } else {
+      L = L + T * background(S, d, lc);
+    }
+    if (cont) {
+      alive = true;
+      ro = make_float4(o.x, o.y, o.z, __uint_as_float(g));
+      rd = make_float4(d.x, d.y, d.z, __uint_as_float(k));
+      thr = make_float4(T.x, T.y, T.z, 0.0f);
+      rad = make_float4(L.x, L.y, L.z, 0.0f);
+      rs = make_uint4((uint32_t)rng.s0, (uint32_t)(rng.s0 >> 32), (uint32_t)rng.s1, (uint32_t)(rng.s1 >> 32));
+    } else {
+      results[g] = make_float4(L.x, L.y, L.z, __uint_as_float(k));
+      need = true;
+      nsample = 1;
+    }
+  }
+  // regenerate finished slots from the work counter (one atomic per wave)
+  const unsigned long long need_mask = __ballot(need);
+  uint32_t wbase = 0;
+  if (lane_id() == 0 && need_mask) wbase = atomicAdd(&ctrl->next_work, (uint32_t)__popcll(need_mask));
+  wbase = __shfl(wbase, 0, 64);
+  if (need) {
+    uint32_t g = wbase + lane_rank(need_mask);
+    if (g < rp.G) {
+      gen_work(cam, rp, g, ro, rd, rs);
+      thr = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+      rad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      alive = true;
+    }
+  }
+  // compact survivors + new paths into the next pool
+  const unsigned long long alive_mask = __ballot(alive);
+  uint32_t obase = 0;
+  if (lane_id() == 0 && alive_mask) obase = atomicAdd(&ctrl->active[cur ^ 1], (uint32_t)__popcll(alive_mask));
+  obase = __shfl(obase, 0, 64);
+  if (alive) {
+    uint32_t pos = obase + lane_rank(alive_mask);
+    out.ro[pos] = ro;
+    out.rd[pos] = rd;
+    out.thr[pos] = thr;
+    out.rad[pos] = rad;
+    out.rng[pos] = rs;
+  }
+  if (COUNT) flush_counters(cnt, lc, 0, 0, nsample, nbounce);
+}
+
+// Image::merge in sample order: acc = ((acc + s0) + s1) + ...
+__global__ __launch_bounds__(kBlock) void k_accumulate(const float4* results, uint32_t n_pix, uint32_t n_samples,
+                                                       const uint32_t* pixlist, float* accum_rgb,
+                                                       uint32_t* accum_bounces) {
+  uint32_t lp = blockIdx.x * kBlock + threadIdx.x;
+  if (lp >= n_pix) return;
+  uint32_t p = pixlist[lp];
+  float r = accum_rgb[3 * (size_t)p], g = accum_rgb[3 * (size_t)p + 1], b = accum_rgb[3 * (size_t)p + 2];
+  uint32_t k = accum_bounces[p];
+  for (uint32_t s = 0; s < n_samples; ++s) {
+    float4 q = results[(size_t)s * n_pix + lp];
+    r = r + q.x;
+    g = g + q.y;
+    b = b + q.z;
+    k += __float_as_uint(q.w);
+  }
+  accum_rgb[3 * (size_t)p] = r;
+  accum_rgb[3 * (size_t)p + 1] = g;
+  accum_rgb[3 * (size_t)p + 2] = b;
+  accum_bounces[p] = k;
+}
+
+// Parity entry point: closest hit of arbitrary rays.
+__global__ __launch_bounds__(kBlock) void k_trace_rays(DevScene S, const float* rays, uint32_t n, float tmin,
+                                                       float tmax, uint4* out, DevCounters* cnt) {
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  LocalCounters lc;
+  uint32_t seg = 0, nh = 0;
+  if (i < n) {
+    V3 o{rays[6 * (size_t)i], rays[6 * (size_t)i + 1], rays[6 * (size_t)i + 2]};
+    V3 d{rays[6 * (size_t)i + 3], rays[6 * (size_t)i + 4], rays[6 * (size_t)i + 5]};
+    Hit h = closest_hit<true>(S, o, d, tmin, tmax, lc);
+    uint32_t front = 0;
+    if (h.prim != kRefNone) front = resolve_hit(S, o, d, h).front_face ? 1u : 0u;
+    out[i] = make_uint4(h.prim, h.container, __float_as_uint(h.prim != kRefNone ? h.t : 0.0f), front);
+    seg = 1;
+    nh = h.prim != kRefNone;
+  }
+  flush_counters(cnt, lc, seg, nh, 0, 0);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+struct mrt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // scene
+  void* scene_mem = nullptr;
+  size_t scene_bytes = 0;
+  DevScene S{};
+  bool has_scene = false;
+  DevCamera cam{};
+  bool has_camera = false;
+  // render state
+  size_t pool_cap = 0;
+  void* pool_mem = nullptr;
+  PathBufs bufs[2]{};
+  uint4* hits = nullptr;
+  float4* results = nullptr;
+  size_t results_cap = 0;
+  Ctrl* ctrl = nullptr;
+  DevCounters* d_cnt = nullptr;
+  Ctrl* h_status = nullptr;  // pinned, 2 slots
+  hipEvent_t ev[2]{};
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t*, uint32_t>> pixlists;
+  // host-buffer render staging
+  float* d_acc_rgb = nullptr;
+  uint32_t* d_acc_b = nullptr;
+  size_t acc_cap = 0;
+  // device ray buffer for mrt_trace_rays
+  float* d_rays = nullptr;
+  uint4* d_rhits = nullptr;
+  size_t rays_cap = 0;
+};
+
+static thread_local std::string g_last_error;
+
+namespace {
+
+void set_device(mrt_ctx* c) { HIP_CHECK(hipSetDevice(c->device)); }
+
+template <typename F>
+int guarded(mrt_ctx* c, F&& f) {
+  if (!c) {
+    g_last_error = "null context";
+    return MRT_ERR_INVALID;
+  }
+  try {
+    set_device(c);
+    f();
+    c->err.clear();
+    return MRT_OK;
+  } catch (const ApiError& e) {
+    c->err = e.msg;
+    return e.code;
+  } catch (const HipError& e) {
+    c->err = e.msg;
+    return MRT_ERR_HIP;
+  } catch (const std::bad_alloc&) {
+    c->err = "out of host memory";
+    return MRT_ERR_NOMEM;
+  } catch (const std::exception& e) {
+    c->err = e.what();
+    return MRT_ERR_INVALID;
+  }
+}
+
+template <typename T>
+size_t align_up(size_t x) {
+  return (x + 255) & ~(size_t)255;
+}
+
+void ensure_pool(mrt_ctx* c, size_t P) {
+  if (P <= c->pool_cap) return;
+  if (c->pool_mem) HIP_CHECK(hipFree(c->pool_mem));
+  c->pool_mem = nullptr;
+  size_t per = 16 * (2 * 5 + 1);  // two state sets + hits
+  HIP_CHECK(hipMalloc(&c->pool_mem, per * P + 4096));
+  char* p = (char*)c->pool_mem;
+  auto take = [&](size_t bytes) {
+    char* r = p;
+    p += (bytes + 255) & ~(size_t)255;
+    return r;
+  };
+  for (int b = 0; b < 2; ++b) {
+    c->bufs[b].ro = (float4*)take(16 * P);
+    c->bufs[b].rd = (float4*)take(16 * P);
+    c->bufs[b].thr = (float4*)take(16 * P);
+    c->bufs[b].rad = (float4*)take(16 * P);
+    c->bufs[b].rng = (uint4*)take(16 * P);
+  }
+  c->hits = (uint4*)take(16 * P);
+  c->pool_cap = P;
+}
+
+void ensure_results(mrt_ctx* c, size_t n) {
+  if (n <= c->results_cap) return;
+  if (c->results) HIP_CHECK(hipFree(c->results));
+  c->results = nullptr;
+  HIP_CHECK(hipMalloc(&c->results, 16 * n));
+  c->results_cap = n;
+}
+
+std::pair<uint32_t*, uint32_t> pixlist(mrt_ctx* c, uint32_t W, uint32_t H, uint32_t si, uint32_t sc) {
+  auto key = std::make_tuple(W, H, si, sc);
+  auto it = c->pixlists.find(key);
+  if (it != c->pixlists.end()) return it->second;
+  // MRT_TILE x MRT_TILE tiles in raster order; this shard owns t % sc == si;
+  // pixels of a tile in raster order, y = 0 the bottom row (main.rs:253-263)
+  uint32_t tx = (W + MRT_TILE - 1) / MRT_TILE, ty = (H + MRT_TILE - 1) / MRT_TILE;
+  std::vector<uint32_t> list;
+  for (uint32_t t = si; t < tx * ty; t += sc) {
+    uint32_t bx = (t % tx) * MRT_TILE, by = (t / tx) * MRT_TILE;
+    for (uint32_t py = 0; py < MRT_TILE; ++py)
+      for (uint32_t px = 0; px < MRT_TILE; ++px) {
+        uint32_t x = bx + px, y = by + py;
+        if (x < W && y < H) list.push_back(y * W + x);
+      }
+  }
+  uint32_t* d = nullptr;
+  if (!list.empty()) {
+    HIP_CHECK(hipMalloc(&d, list.size() * 4));
+    HIP_CHECK(hipMemcpy(d, list.data(), list.size() * 4, hipMemcpyHostToDevice));
+  }
+  auto v = std::make_pair(d, (uint32_t)list.size());
+  c->pixlists[key] = v;
+  return v;
+}
+
+void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t* d_b, hipStream_t st) {
+  if (!a) throw ApiError{MRT_ERR_INVALID, "null render args"};
+  if (!c->has_scene) throw ApiError{MRT_ERR_STATE, "no scene uploaded"};
+  if (!c->has_camera) throw ApiError{MRT_ERR_STATE, "no camera set"};
+  if (a->width == 0 || a->height == 0) throw ApiError{MRT_ERR_INVALID, "empty image"};
+  if ((uint64_t)a->width * a->height >= (1ull << 32)) throw ApiError{MRT_ERR_INVALID, "image too large"};
+  uint32_t sc = a->shard_count ? a->shard_count : 1;
+  if (a->shard_index >= sc) throw ApiError{MRT_ERR_INVALID, "shard_index >= shard_count"};
+  if (a->spp_count == 0) return;
+  if ((uint64_t)a->spp_begin + a->spp_count > 0xFFFFFFFFull) throw ApiError{MRT_ERR_INVALID, "sample index overflow"};
+  auto pl = pixlist(c, a->width, a->height, a->shard_index, sc);
+  const uint32_t n_pix = pl.second;
+  if (n_pix == 0) return;
+  const bool count = (a->flags & MRT_RENDER_COUNTERS) != 0;
+  // results slab <= 64M samples (1 GiB); pool <= 2M paths
+  uint32_t spp_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(a->spp_count, (64ull << 20) / n_pix));
+  const size_t pool = std::min<size_t>((size_t)n_pix * spp_chunk, (size_t)2 << 20);
+  ensure_pool(c, pool);
+  ensure_results(c, (size_t)n_pix * spp_chunk);
+  for (uint32_t done = 0; done < a->spp_count; done += spp_chunk) {
+    uint32_t cs = std::min(spp_chunk, a->spp_count - done);
+    RenderParams rp;
+    rp.W = a->width;
+    rp.H = a->height;
+    rp.seed = a->seed;
+    rp.max_depth = a->max_depth;
+    rp.n_pix = n_pix;
+    rp.G = n_pix * cs;
+    rp.sample_base = a->spp_begin + done;
+    rp.pixlist = pl.first;
+    if (a->max_depth == 0) {
+      // trace(ray, 0) returns (0, 0) for every sample: nothing to add
+      continue;
+    }
+    uint32_t n0 = (uint32_t)std::min<size_t>(rp.G, c->pool_cap);
+    Ctrl init{{n0, 0}, n0, 0};
+    HIP_CHECK(hipMemcpyAsync(c->ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_generate, dim3((n0 + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c->cam, rp, c->bufs[0], n0);
+    HIP_CHECK(hipGetLastError());
+    const uint32_t grid = (uint32_t)((c->pool_cap + kBlock - 1) / kBlock);
+    const int kBatch = 4;
+    uint32_t it = 0;
+    int slot = 0;
+    bool pending = false;
+    for (;;) {
+      for (int b = 0; b < kBatch; ++b, ++it) {
+        uint32_t cur = it & 1;
+        if (count) {
+          hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(kBlock), 0, st, c->S, c->bufs[cur], c->hits, c->ctrl,
+                             cur, c->d_cnt);
+          hipLaunchKernelGGL(k_shade<true>, dim3(grid), dim3(kBlock), 0, st, c->S, c->cam, rp, c->bufs[cur],
+                             c->bufs[cur ^ 1], (const uint4*)c->hits, c->ctrl, cur, c->results, c->d_cnt);
+        } else {
+          hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(kBlock), 0, st, c->S, c->bufs[cur], c->hits, c->ctrl,
+                             cur, c->d_cnt);
+          hipLaunchKernelGGL(k_shade<false>, dim3(grid), dim3(kBlock), 0, st, c->S, c->cam, rp, c->bufs[cur],
+                             c->bufs[cur ^ 1], (const uint4*)c->hits, c->ctrl, cur, c->results, c->d_cnt);
+        }
+        HIP_CHECK(hipGetLastError());
+      }
+      HIP_CHECK(hipMemcpyAsync(&c->h_status[slot], c->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, st));
+      HIP_CHECK(hipEventRecord(c->ev[slot], st));
+      if (pending) {
+        HIP_CHECK(hipEventSynchronize(c->ev[slot ^ 1]));
+        const Ctrl& s = c->h_status[slot ^ 1];
+        // status after an even number of iterations: the live pool is active[0]
+        if (s.active[0] == 0 && s.next_work >= rp.G) break;
+      }
+      pending = true;
+      slot ^= 1;
+      if (it > 64u * 1024u) throw ApiError{MRT_ERR_HIP, "render did not converge"};
+    }
+    hipLaunchKernelGGL(k_accumulate, dim3((n_pix + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
+                       (const float4*)c->results, n_pix, cs, (const uint32_t*)pl.first, d_rgb, d_b);
+    HIP_CHECK(hipGetLastError());
+  }
+  if (count) {
+    // samples/segments for max_depth == 0 are not traced; nothing to add
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mrt_abi_version(void) { return MRT_ABI_VERSION; }
+const char* mrt_global_last_error(void) { return g_last_error.c_str(); }
+const char* mrt_last_error(const mrt_ctx* c) { return c ? c->err.c_str() : g_last_error.c_str(); }
+
+int mrt_create(int device, mrt_ctx** out) {
+  if (!out) {
+    g_last_error = "null output pointer";
+    return MRT_ERR_INVALID;
+  }
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    g_last_error = "no HIP device available (the massrt hot path has no CPU fallback)";
+    return MRT_ERR_HIP;
+  }
+  if (device < 0 || device >= n) {
+    g_last_error = "device ordinal out of range";
+    return MRT_ERR_INVALID;
+  }
+  mrt_ctx* c = new mrt_ctx();
+  c->device = device;
+  int rc = guarded(c, [&] {
+    HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_CHECK(hipMalloc(&c->ctrl, sizeof(Ctrl)));
+    HIP_CHECK(hipMalloc(&c->d_cnt, sizeof(DevCounters)));
+    HIP_CHECK(hipMemset(c->d_cnt, 0, sizeof(DevCounters)));
+    HIP_CHECK(hipHostMalloc(&c->h_status, 2 * sizeof(Ctrl), hipHostMallocDefault));
+    HIP_CHECK(hipEventCreateWithFlags(&c->ev[0], hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&c->ev[1], hipEventDisableTiming));
+  });
+  if (rc != MRT_OK) {
+    g_last_error = c->err;
+    mrt_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return MRT_OK;
+}
+
+int mrt_destroy(mrt_ctx* c) {
+  if (!c) return MRT_OK;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  hipFree(c->scene_mem);
+  hipFree(c->pool_mem);
+  hipFree(c->results);
+  hipFree(c->ctrl);
+  hipFree(c->d_cnt);
+  hipFree(c->d_acc_rgb);
+  hipFree(c->d_acc_b);
+  hipFree(c->d_rays);
+  hipFree(c->d_rhits);
+  for (auto& kv : c->pixlists) hipFree(kv.second.first);
+  if (c->h_status) hipHostFree(c->h_status);
+  if (c->ev[0]) hipEventDestroy(c->ev[0]);
+  if (c->ev[1]) hipEventDestroy(c->ev[1]);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+  return MRT_OK;
+}
+
+int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
+  return guarded(c, [&] {
+    if (!d) throw ApiError{MRT_ERR_INVALID, "null scene"};
+    HostScene hs;
+    std::string err;
+    if (!build_host_scene(*d, hs, err)) throw ApiError{MRT_ERR_INVALID, err};
+    // one allocation, 256-B aligned sections
+    size_t off = 0;
+    auto sec = [&](size_t bytes) {
+      size_t o = off;
+      off += (bytes + 255) & ~(size_t)255;
+      return o;
+    };
+    size_t o_slots = sec(hs.slots.size() * 4), o_inv = sec(hs.inst_inv.size() * 4),
+           o_fwd = sec(hs.inst_fwd.size() * 4), o_imat = sec(hs.inst_mat.size() * 4),
+           o_mmat = sec(hs.model_mat.size() * 4), o_sph = sec(hs.sph.size() * 4), o_smat = sec(hs.sph_mat.size() * 4),
+           o_tri = sec(hs.tri_shade.size() * 4), o_mat = sec(hs.materials.size() * sizeof(GpuMaterial)),
+           o_tex = sec(hs.textures.size() * sizeof(GpuTexture)), o_texel = sec(hs.texels.size() * 4);
+    if (c->scene_mem) HIP_CHECK(hipFree(c->scene_mem));
+    c->scene_mem = nullptr;
+    c->has_scene = false;
+    HIP_CHECK(hipMalloc(&c->scene_mem, off + 256));
+    char* base = (char*)c->scene_mem;
+    auto up = [&](size_t o, const void* src, size_t bytes) {
+      if (bytes) HIP_CHECK(hipMemcpy(base + o, src, bytes, hipMemcpyHostToDevice));
+    };
+    up(o_slots, hs.slots.data(), hs.slots.size() * 4);
+    up(o_inv, hs.inst_inv.data(), hs.inst_inv.size() * 4);
+    up(o_fwd, hs.inst_fwd.data(), hs.inst_fwd.size() * 4);
+    up(o_imat, hs.inst_mat.data(), hs.inst_mat.size() * 4);
+    up(o_mmat, hs.model_mat.data(), hs.model_mat.size() * 4);
+    up(o_sph, hs.sph.data(), hs.sph.size() * 4);
+    up(o_smat, hs.sph_mat.data(), hs.sph_mat.size() * 4);
+    up(o_tri, hs.tri_shade.data(), hs.tri_shade.size() * 4);
+    up(o_mat, hs.materials.data(), hs.materials.size() * sizeof(GpuMaterial));
+    up(o_tex, hs.textures.data(), hs.textures.size() * sizeof(GpuTexture));
+    up(o_texel, hs.texels.data(), hs.texels.size() * 4);
+    DevScene S{};
+    S.slots = (const uint32_t*)(base + o_slots);
+    S.world_begin = hs.world_begin;
+    S.world_end = hs.world_end;
+    S.inst_inv = (const float*)(base + o_inv);
+    S.inst_fwd = (const float*)(base + o_fwd);
+    S.inst_mat = (const uint32_t*)(base + o_imat);
+    S.model_mat = (const uint32_t*)(base + o_mmat);
+    S.sph = (const float*)(base + o_sph);
+    S.sph_mat = (const uint32_t*)(base + o_smat);
+    S.tri_shade = (const float*)(base + o_tri);
+    S.materials = (const GpuMaterial*)(base + o_mat);
+    S.textures = (const GpuTexture*)(base + o_tex);
+    S.texels = (const uint32_t*)(base + o_texel);
+    S.bg_kind = hs.bg_kind;
+    S.bg_texture = hs.bg_texture;
+    S.bg_surf_kind = hs.bg_surf_kind;
+    for (int k = 0; k < 4; ++k) S.bg_color[k] = hs.bg_color[k];
+    c->S = S;
+    c->scene_bytes = off;
+    c->has_scene = true;
+  });
+}
+
+int mrt_scene_device_bytes(mrt_ctx* c, uint64_t* out) {
+  return guarded(c, [&] {
+    if (!out) throw ApiError{MRT_ERR_INVALID, "null output"};
+    *out = c->scene_bytes;
+  });
+}
+
+int mrt_set_camera(mrt_ctx* c, const mrt_camera* cam) {
+  return guarded(c, [&] {
+    if (!cam) throw ApiError{MRT_ERR_INVALID, "null camera"};
+    DevCamera d;
+    d.origin = V3{cam->origin[0], cam->origin[1], cam->origin[2]};
+    d.llc = V3{cam->lower_left_corner[0], cam->lower_left_corner[1], cam->lower_left_corner[2]};
+    d.horizontal = V3{cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]};
+    d.vertical = V3{cam->vertical[0], cam->vertical[1], cam->vertical[2]};
+    d.u = V3{cam->u[0], cam->u[1], cam->u[2]};
+    d.v = V3{cam->v[0], cam->v[1], cam->v[2]};
+    d.lens_radius = cam->lens_radius;
+    c->cam = d;
+    c->has_camera = true;
+  });
+}
+
+int mrt_render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t* d_b, void* stream) {
+  return guarded(c, [&] {
+    if (!d_rgb || !d_b) throw ApiError{MRT_ERR_INVALID, "null accumulation buffer"};
+    render_device(c, a, d_rgb, d_b, stream ? (hipStream_t)stream : c->stream);
+  });
+}
+
+int mrt_render(mrt_ctx* c, const mrt_render_args* a, float* rgb, uint32_t* bounces) {
+  return guarded(c, [&] {
+    if (!a || !rgb || !bounces) throw ApiError{MRT_ERR_INVALID, "null argument"};
+    size_t np = (size_t)a->width * a->height;
+    if (np > c->acc_cap) {
+      hipFree(c->d_acc_rgb);
+      hipFree(c->d_acc_b);
+      c->d_acc_rgb = nullptr;
+      c->d_acc_b = nullptr;
+      HIP_CHECK(hipMalloc(&c->d_acc_rgb, np * 12));
+      HIP_CHECK(hipMalloc(&c->d_acc_b, np * 4));
+      c->acc_cap = np;
+    }
+    HIP_CHECK(hipMemcpyAsync(c->d_acc_rgb, rgb, np * 12, hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(hipMemcpyAsync(c->d_acc_b, bounces, np * 4, hipMemcpyHostToDevice, c->stream));
+    render_device(c, a, c->d_acc_rgb, c->d_acc_b, c->stream);
+    HIP_CHECK(hipMemcpyAsync(rgb, c->d_acc_rgb, np * 12, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipMemcpyAsync(bounces, c->d_acc_b, np * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+  });
+}
+
+int mrt_trace_rays(mrt_ctx* c, const float* rays, uint32_t n, float t_min, float t_max, mrt_hit* out) {
+  return guarded(c, [&] {
+    if (!c->has_scene) throw ApiError{MRT_ERR_STATE, "no scene uploaded"};
+    if (n == 0) return;
+    if (!rays || !out) throw ApiError{MRT_ERR_INVALID, "null argument"};
+    if (n > c->rays_cap) {
+      hipFree(c->d_rays);
+      hipFree(c->d_rhits);
+      c->d_rays = nullptr;
+      c->d_rhits = nullptr;
+      HIP_CHECK(hipMalloc(&c->d_rays, (size_t)n * 24));
+      HIP_CHECK(hipMalloc(&c->d_rhits, (size_t)n * 16));
+      c->rays_cap = n;
+    }
+    HIP_CHECK(hipMemcpyAsync(c->d_rays, rays, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_trace_rays, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, c->S,
+                       (const float*)c->d_rays, n, t_min, t_max, c->d_rhits, c->d_cnt);
+    HIP_CHECK(hipGetLastError());
+    std::vector<uint4> h(n);
+    HIP_CHECK(hipMemcpyAsync(h.data(), c->d_rhits, (size_t)n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    for (uint32_t i = 0; i < n; ++i) {
+      out[i].prim = h[i].x;
+      out[i].container = h[i].y;
+      memcpy(&out[i].t, &h[i].z, 4);
+      out[i].front_face = h[i].w;
+    }
+  });
+}
+
+int mrt_get_counters(mrt_ctx* c, mrt_counters* out) {
+  return guarded(c, [&] {
+    if (!out) throw ApiError{MRT_ERR_INVALID, "null output"};
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    HIP_CHECK(hipDeviceSynchronize());
+    DevCounters h;
+    HIP_CHECK(hipMemcpy(&h, c->d_cnt, sizeof(h), hipMemcpyDeviceToHost));
+    out->samples = h.samples;
+    out->segments = h.segments;
+    out->node_visits = h.node_visits;
+    out->sphere_tests = h.sphere_tests;
+    out->triangle_tests = h.triangle_tests;
+    out->instance_entries = h.instance_entries;
+    out->model_entries = h.model_entries;
+    out->closest_hits = h.closest_hits;
+    out->texel_taps = h.texel_taps;
+    out->bounces = h.bounces;
+  });
+}
+
+int mrt_reset_counters(mrt_ctx* c) {
+  return guarded(c, [&] {
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipMemset(c->d_cnt, 0, sizeof(DevCounters)));
+  });
+}
+
+}  // extern "C"

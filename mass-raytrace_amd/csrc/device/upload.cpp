@@ -1,0 +1,251 @@
+// upload.cpp — linearise the reference BVH into the preorder slot stream.
+#include "upload.h"
+
+#include <string.h>
+
+#include <unordered_map>
+
+namespace mrt {
+
+namespace {
+
+uint32_t fbits(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return u;
+}
+
+struct Emitter {
+  const mrt_scene_desc& d;
+  HostScene& s;
+  std::string& err;
+  // instance/model records whose BLAS range is patched after the BLAS regions
+  std::vector<std::pair<uint32_t, uint32_t>> jump_patches;  // (slot index, blas root node)
+
+  uint32_t n_slots() const { return (uint32_t)(s.slots.size() / 4); }
+  uint32_t push_slot(uint32_t a, uint32_t b, uint32_t c, uint32_t w) {
+    uint32_t i = n_slots();
+    s.slots.push_back(a), s.slots.push_back(b), s.slots.push_back(c), s.slots.push_back(w);
+    return i;
+  }
+
+  bool emit_prim(uint32_t ref, bool in_blas) {
+    uint32_t kind = MRT_REF_KIND(ref), idx = MRT_REF_INDEX(ref);
+    switch (kind) {
+      case MRT_REF_SPHERE: {
+        if (idx >= d.n_spheres) return fail("sphere index out of range");
+        const mrt_sphere& sp = d.spheres[idx];
+        push_slot(fbits(sp.center[0]), fbits(sp.center[1]), fbits(sp.center[2]), fbits(sp.radius));
+        push_slot(idx, 0, 0, KIND_SPHERE);
+        s.n_prim_records++;
+        return true;
+      }
+      case MRT_REF_TRIANGLE: {
+        if (idx >= d.n_triangles) return fail("triangle index out of range");
+        const mrt_triangle& t = d.triangles[idx];
+        float ab[3], ac[3];
+        for (int k = 0; k < 3; ++k) ab[k] = t.b[k] - t.a[k], ac[k] = t.c[k] - t.a[k];
+        uint32_t flags = 0;
+        if (t.flags & MRT_TRI_HAS_UV) flags |= TRI_FLAG_UV;
+        if (needs_alpha(t)) flags |= TRI_FLAG_ALPHA;
+        push_slot(fbits(t.a[0]), fbits(t.a[1]), fbits(t.a[2]), fbits(ab[0]));
+        push_slot(fbits(ab[1]), fbits(ab[2]), idx, KIND_TRI);
+        push_slot(fbits(ac[0]), fbits(ac[1]), fbits(ac[2]), flags);
+        s.n_prim_records++;
+        return true;
+      }
+      case MRT_REF_INSTANCE:
+      case MRT_REF_MODEL: {
+        if (in_blas) return fail("instances/models cannot be nested inside a BLAS");
+        uint32_t root;
+        if (kind == MRT_REF_INSTANCE) {
+          if (idx >= d.n_instances) return fail("instance index out of range");
+          root = d.instances[idx].blas_root;
+        } else {
+          if (idx >= d.n_models) return fail("model index out of range");
+          root = d.models[idx].blas_root;
+        }
+        if (root >= d.n_nodes) return fail("BLAS root out of range");
+        uint32_t at = push_slot(idx, 0, 0, 0);
+        push_slot(0, 0, 0, kind == MRT_REF_INSTANCE ? KIND_INST : KIND_MODEL);
+        jump_patches.push_back({at, root});
+        s.n_prim_records++;
+        return true;
+      }
+      default:
+        return fail("bad child reference kind");
+    }
+  }
+
+  // Triangle::intersect runs alpha_test only with uvs; it can reject only if
+  // the triangle's own material samples a texture holding a zero alpha.
+  bool needs_alpha(const mrt_triangle& t) const {
+    if (!(t.flags & MRT_TRI_HAS_UV) || t.material >= d.n_materials) return false;
+    const mrt_material& m = d.materials[t.material];
+    if (m.kind != MRT_MAT_LAMBERTIAN && m.kind != MRT_MAT_METAL) return false;
+    if (m.surface >= d.n_surfaces) return false;
+    const mrt_surface& sf = d.surfaces[m.surface];
+    if (sf.kind == MRT_SURF_SOLID) return sf.color[3] == 0.0f;
+    if (sf.texture >= d.n_textures) return false;
+    const mrt_texture& tx = d.textures[sf.texture];
+    for (size_t i = 0; i < (size_t)tx.width * tx.height; ++i)
+      if (tx.rgba[4 * i + 3] == 0) return true;
+    return false;
+  }
+
+  bool fail(const char* m) {
+    err = m;
+    return false;
+  }
+
+  // Preorder emission of the subtree under `ref` with an explicit stack.
+  bool emit_tree(uint32_t ref, bool in_blas) {
+    struct Frame {
+      uint32_t ref;
+      uint32_t box_slot;  // != ~0: close (patch skip of) this box
+    };
+    std::vector<Frame> stack;
+    stack.push_back({ref, ~0u});
+    uint32_t depth_guard = 0;
+    while (!stack.empty()) {
+      Frame f = stack.back();
+      stack.pop_back();
+      if (f.box_slot != ~0u) {
+        s.slots[4 * (f.box_slot + 1) + 2] = n_slots();  // skip = first slot after subtree
+        continue;
+      }
+      if (MRT_REF_KIND(f.ref) != MRT_REF_NODE) {
+        if (!emit_prim(f.ref, in_blas)) return false;
+        continue;
+      }
+      uint32_t idx = MRT_REF_INDEX(f.ref);
+      if (idx >= d.n_nodes) return fail("node index out of range");
+      if (++depth_guard > 4 * d.n_nodes + 16) return fail("BVH is not a tree (cycle)");
+      const mrt_node& n = d.nodes[idx];
+      uint32_t at = push_slot(fbits(n.min[0]), fbits(n.min[1]), fbits(n.min[2]), fbits(n.max[0]));
+      push_slot(fbits(n.max[1]), fbits(n.max[2]), 0, KIND_BOX);
+      s.n_box_records++;
+      stack.push_back({0, at});  // closes after both children
+      if (MRT_REF_KIND(n.right) != MRT_REF_NONE) stack.push_back({n.right, ~0u});
+      if (MRT_REF_KIND(n.left) == MRT_REF_NONE) return fail("BvhNode without a left child");
+      stack.push_back({n.left, ~0u});
+      if (stack.size() > s.max_depth) s.max_depth = (uint32_t)stack.size();
+    }
+    return true;
+  }
+};
+
+void put_m4_12(std::vector<float>& dst, const float* m16) {
+  // column-major 4x4 -> c0.xyz c1.xyz c2.xyz c3.xyz
+  for (int c = 0; c < 4; ++c)
+    for (int r = 0; r < 3; ++r) dst.push_back(m16[4 * c + r]);
+}
+
+}  // namespace
+
+bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
+  s = HostScene{};
+  Emitter e{d, s, err, {}};
+  // materials
+  for (uint32_t i = 0; i < d.n_materials; ++i) {
+    const mrt_material& m = d.materials[i];
+    GpuMaterial g{};
+    g.kind = m.kind;
+    g.param = m.param;
+    if (m.kind > MRT_MAT_DIFFUSE_LIGHT) return (err = "bad material kind", false);
+    if (m.kind == MRT_MAT_LAMBERTIAN || m.kind == MRT_MAT_METAL) {
+      if (m.surface >= d.n_surfaces) return (err = "material surface out of range", false);
+      const mrt_surface& sf = d.surfaces[m.surface];
+      g.surf_kind = sf.kind;
+      g.texture = sf.texture;
+      if (sf.kind == MRT_SURF_TEXTURE && sf.texture >= d.n_textures) return (err = "surface texture out of range", false);
+      for (int k = 0; k < 4; ++k) g.color[k] = sf.color[k];
+    } else if (m.kind == MRT_MAT_DIFFUSE_LIGHT) {
+      for (int k = 0; k < 3; ++k) g.color[k] = m.emit[k];
+    }
+    s.materials.push_back(g);
+  }
+  // textures
+  for (uint32_t i = 0; i < d.n_textures; ++i) {
+    const mrt_texture& t = d.textures[i];
+    if (t.wrap == MRT_WRAP_MIRROR) return (err = "WrapMode::Mirror is unimplemented (texture.rs:280-282)", false);
+    if (t.wrap != MRT_WRAP_REPEAT && t.wrap != MRT_WRAP_CLAMP) return (err = "bad wrap mode", false);
+    if (t.width == 0 || t.height == 0 || !t.rgba) return (err = "empty texture", false);
+    GpuTexture g{t.width, t.height, t.wrap, (uint32_t)s.texels.size()};
+    s.textures.push_back(g);
+    size_t n = (size_t)t.width * t.height;
+    size_t base = s.texels.size();
+    s.texels.resize(base + n);
+    memcpy(&s.texels[base], t.rgba, n * 4);
+  }
+  auto check_mat = [&](uint32_t m, bool allow_none) {
+    return (allow_none && m == MRT_NO_MATERIAL) || m < d.n_materials;
+  };
+  // spheres
+  for (uint32_t i = 0; i < d.n_spheres; ++i) {
+    const mrt_sphere& sp = d.spheres[i];
+    if (!check_mat(sp.material, false)) return (err = "sphere material out of range", false);
+    for (int k = 0; k < 3; ++k) s.sph.push_back(sp.center[k]);
+    s.sph.push_back(sp.radius);
+    s.sph_mat.push_back(sp.material);
+  }
+  // triangles (shading records)
+  s.tri_shade.reserve((size_t)d.n_triangles * kTriShadeQuads * 4);
+  for (uint32_t i = 0; i < d.n_triangles; ++i) {
+    const mrt_triangle& t = d.triangles[i];
+    if (!check_mat(t.material, false)) return (err = "triangle material out of range", false);
+    float q[28] = {t.a[0],   t.a[1],   t.a[2],   t.b[0],   t.b[1],   t.b[2],   t.c[0],
+                   t.c[1],   t.c[2],   t.na[0],  t.na[1],  t.na[2],  t.nb[0],  t.nb[1],
+                   t.nb[2],  t.nc[0],  t.nc[1],  t.nc[2],  t.uva[0], t.uva[1], t.uvb[0],
+                   t.uvb[1], t.uvc[0], t.uvc[1], 0,        0,        0,        0};
+    uint32_t flags = (t.flags & MRT_TRI_HAS_UV) ? TRI_FLAG_UV : 0;
+    memcpy(&q[24], &t.material, 4);
+    memcpy(&q[25], &flags, 4);
+    s.tri_shade.insert(s.tri_shade.end(), q, q + 28);
+  }
+  // instances / models
+  for (uint32_t i = 0; i < d.n_instances; ++i) {
+    const mrt_instance& in = d.instances[i];
+    if (!check_mat(in.material, true)) return (err = "instance material out of range", false);
+    put_m4_12(s.inst_inv, in.inv);
+    put_m4_12(s.inst_fwd, in.fwd);
+    s.inst_mat.push_back(in.material);
+  }
+  for (uint32_t i = 0; i < d.n_models; ++i) {
+    if (!check_mat(d.models[i].material, true)) return (err = "model material out of range", false);
+    s.model_mat.push_back(d.models[i].material);
+  }
+  // background
+  s.bg_kind = d.background.kind;
+  for (int k = 0; k < 3; ++k) s.bg_color[k] = d.background.color[k];
+  if (d.background.kind == MRT_BG_SKYSPHERE) {
+    if (d.background.surface >= d.n_surfaces) return (err = "background surface out of range", false);
+    const mrt_surface& sf = d.background.surface < d.n_surfaces ? d.surfaces[d.background.surface] : mrt_surface{};
+    s.bg_surf_kind = sf.kind;
+    s.bg_texture = sf.texture;
+    if (sf.kind == MRT_SURF_TEXTURE && sf.texture >= d.n_textures) return (err = "background texture out of range", false);
+    for (int k = 0; k < 4; ++k) s.bg_color[k] = sf.color[k];
+  } else if (d.background.kind > MRT_BG_SKYSPHERE) {
+    return (err = "bad background kind", false);
+  }
+  // world region: World::objects in order
+  s.world_begin = 0;
+  for (uint32_t r = 0; r < d.n_roots; ++r)
+    if (!e.emit_tree(d.roots[r], false)) return false;
+  s.world_end = e.n_slots();
+  // BLAS regions, one per distinct root, emitted once and shared
+  std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> blas;
+  for (auto& p : e.jump_patches) {
+    auto it = blas.find(p.second);
+    if (it == blas.end()) {
+      uint32_t b = e.n_slots();
+      if (!e.emit_tree(MRT_REF(MRT_REF_NODE, p.second), true)) return false;
+      it = blas.emplace(p.second, std::make_pair(b, e.n_slots())).first;
+    }
+    s.slots[4 * p.first + 1] = it->second.first;
+    s.slots[4 * p.first + 2] = it->second.second;
+  }
+  return true;
+}
+
+}  // namespace mrt

@@ -1,0 +1,31 @@
+// upload.h — mrt_scene_desc (reference tree) -> HBM layout (layout.h).
+#pragma once
+#include <string>
+#include <vector>
+
+#include "../../../include/massrt.h"
+#include "layout.h"
+
+namespace mrt {
+
+struct HostScene {
+  std::vector<uint32_t> slots;  // 4 words per slot
+  uint32_t world_begin = 0, world_end = 0;
+  std::vector<float> inst_inv, inst_fwd;
+  std::vector<uint32_t> inst_mat, model_mat;
+  std::vector<float> sph;
+  std::vector<uint32_t> sph_mat;
+  std::vector<float> tri_shade;
+  std::vector<GpuMaterial> materials;
+  std::vector<GpuTexture> textures;
+  std::vector<uint32_t> texels;
+  uint32_t bg_kind = 0, bg_texture = 0, bg_surf_kind = 0;
+  float bg_color[4] = {0, 0, 0, 0};
+  // statistics
+  uint32_t n_box_records = 0, n_prim_records = 0, max_depth = 0;
+};
+
+// Validates the description and linearises it. Returns false with `err` set.
+bool build_host_scene(const mrt_scene_desc& d, HostScene& out, std::string& err);
+
+}  // namespace mrt

@@ -1,0 +1,449 @@
+"""massrt — ctypes harness over libmassrt.so (include/massrt.h).
+
+Python is only the test/bench driver: the product is the C ABI library (C++
+host scene builder + gfx950 HIP kernels). There is no CPU fallback — creating a
+`Context` without a GPU raises.
+
+Mirrors of the reference surface (file:line under /root/reference/src):
+  Builder.builtin(name)     Scene::generate + World::build_bvh (scenes.rs:25-33, main.rs:107-112)
+  Context.render            render() sample loop + Image::merge (main.rs:150-295, 629-638)
+  Context.trace_rays        World::intersect (world.rs:131-144) on explicit rays
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "libmassrt.so"
+REPO = _HERE.parent.parent
+
+# ---- constants (massrt.h) --------------------------------------------------
+REF_NONE, REF_NODE, REF_SPHERE, REF_TRIANGLE, REF_INSTANCE, REF_MODEL = range(6)
+MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT = range(5)
+WRAP_MIRROR, WRAP_REPEAT, WRAP_CLAMP = range(3)
+BG_SOLID, BG_SKY, BG_SKYSPHERE = range(3)
+NO_MATERIAL = 0xFFFFFFFF
+RENDER_COUNTERS = 1
+MAX_DEPTH = 50  # main.rs:37
+ASPECT_RATIO = np.float32(16.0) / np.float32(9.0)  # main.rs:39 (f32)
+
+
+def ref_kind(r: int) -> int:
+    return int(r) >> 28
+
+
+def ref_index(r: int) -> int:
+    return int(r) & 0x0FFFFFFF
+
+
+class MrtNode(C.Structure):
+    _fields_ = [("min", C.c_float * 3), ("max", C.c_float * 3), ("left", C.c_uint32), ("right", C.c_uint32)]
+
+
+class MrtSphere(C.Structure):
+    _fields_ = [("center", C.c_float * 3), ("radius", C.c_float), ("material", C.c_uint32)]
+
+
+class MrtTriangle(C.Structure):
+    _fields_ = [
+        ("a", C.c_float * 3), ("b", C.c_float * 3), ("c", C.c_float * 3),
+        ("na", C.c_float * 3), ("nb", C.c_float * 3), ("nc", C.c_float * 3),
+        ("uva", C.c_float * 2), ("uvb", C.c_float * 2), ("uvc", C.c_float * 2),
+        ("tangent", C.c_float * 3), ("bitangent", C.c_float * 3),
+        ("material", C.c_uint32), ("flags", C.c_uint32),
+    ]
+
+
+class MrtInstance(C.Structure):
+    _fields_ = [("fwd", C.c_float * 16), ("inv", C.c_float * 16), ("blas_root", C.c_uint32), ("material", C.c_uint32)]
+
+
+class MrtModel(C.Structure):
+    _fields_ = [("blas_root", C.c_uint32), ("material", C.c_uint32)]
+
+
+class MrtMaterial(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("surface", C.c_uint32), ("param", C.c_float), ("emit", C.c_float * 3)]
+
+
+class MrtSurface(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("texture", C.c_uint32), ("color", C.c_float * 4)]
+
+
+class MrtTexture(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("wrap", C.c_uint32), ("rgba", C.POINTER(C.c_uint8))]
+
+
+class MrtBackground(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("surface", C.c_uint32), ("color", C.c_float * 3)]
+
+
+class MrtSceneDesc(C.Structure):
+    _fields_ = [
+        ("nodes", C.POINTER(MrtNode)), ("n_nodes", C.c_uint32),
+        ("roots", C.POINTER(C.c_uint32)), ("n_roots", C.c_uint32),
+        ("spheres", C.POINTER(MrtSphere)), ("n_spheres", C.c_uint32),
+        ("triangles", C.POINTER(MrtTriangle)), ("n_triangles", C.c_uint32),
+        ("instances", C.POINTER(MrtInstance)), ("n_instances", C.c_uint32),
+        ("models", C.POINTER(MrtModel)), ("n_models", C.c_uint32),
+        ("materials", C.POINTER(MrtMaterial)), ("n_materials", C.c_uint32),
+        ("surfaces", C.POINTER(MrtSurface)), ("n_surfaces", C.c_uint32),
+        ("textures", C.POINTER(MrtTexture)), ("n_textures", C.c_uint32),
+        ("background", MrtBackground),
+    ]
+
+
+class MrtCamera(C.Structure):
+    _fields_ = [
+        ("origin", C.c_float * 3), ("lower_left_corner", C.c_float * 3), ("horizontal", C.c_float * 3),
+        ("vertical", C.c_float * 3), ("u", C.c_float * 3), ("v", C.c_float * 3), ("lens_radius", C.c_float),
+    ]
+
+    def fields(self) -> np.ndarray:
+        return np.array(list(self.origin) + list(self.lower_left_corner) + list(self.horizontal)
+                        + list(self.vertical) + list(self.u) + list(self.v) + [self.lens_radius], dtype=np.float32)
+
+
+class MrtRenderArgs(C.Structure):
+    _fields_ = [
+        ("width", C.c_uint32), ("height", C.c_uint32), ("spp_begin", C.c_uint32), ("spp_count", C.c_uint32),
+        ("seed", C.c_uint64), ("max_depth", C.c_uint32), ("shard_index", C.c_uint32), ("shard_count", C.c_uint32),
+        ("flags", C.c_uint32),
+    ]
+
+
+class MrtHit(C.Structure):
+    _fields_ = [("prim", C.c_uint32), ("container", C.c_uint32), ("t", C.c_float), ("front_face", C.c_uint32)]
+
+
+COUNTER_FIELDS = ["samples", "segments", "node_visits", "sphere_tests", "triangle_tests", "instance_entries",
+                  "model_entries", "closest_hits", "texel_taps", "bounces"]
+
+
+class MrtCounters(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in COUNTER_FIELDS]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f in COUNTER_FIELDS}
+
+
+# symbols the header declares (checked by the CPU test-suite)
+EXPORTED_SYMBOLS = [
+    "mrt_create", "mrt_destroy", "mrt_last_error", "mrt_global_last_error", "mrt_abi_version",
+    "mrt_upload_scene", "mrt_set_camera", "mrt_render", "mrt_render_device", "mrt_trace_rays",
+    "mrt_get_counters", "mrt_reset_counters", "mrt_scene_device_bytes",
+    "mrt_builder_new", "mrt_builder_free", "mrt_builder_builtin", "mrt_builder_rand_f32", "mrt_builder_solid",
+    "mrt_builder_texture_png", "mrt_builder_texture_rgba", "mrt_builder_material", "mrt_builder_background",
+    "mrt_builder_add_sphere", "mrt_builder_add_triangle", "mrt_builder_model", "mrt_builder_model_from_ply",
+    "mrt_builder_add_instance", "mrt_builder_camera", "mrt_builder_build_bvh", "mrt_builder_desc",
+    "mrt_builder_last_error", "mrt_load_ply", "mrt_load_stl", "mrt_load_obj",
+]
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libmassrt.so (built by __graft_entry__.build() / make)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(str(LIB_PATH))
+    P, U32, U64, F, I, I64 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_float, C.c_int, C.c_int64
+    fp = C.POINTER(C.c_float)
+    sig = {
+        "mrt_create": (I, [I, C.POINTER(P)]),
+        "mrt_destroy": (I, [P]),
+        "mrt_last_error": (C.c_char_p, [P]),
+        "mrt_global_last_error": (C.c_char_p, []),
+        "mrt_builder_last_error": (C.c_char_p, []),
+        "mrt_abi_version": (I, []),
+        "mrt_upload_scene": (I, [P, C.POINTER(MrtSceneDesc)]),
+        "mrt_set_camera": (I, [P, C.POINTER(MrtCamera)]),
+        "mrt_render": (I, [P, C.POINTER(MrtRenderArgs), fp, C.POINTER(C.c_uint32)]),
+        "mrt_render_device": (I, [P, C.POINTER(MrtRenderArgs), P, P, P]),
+        "mrt_trace_rays": (I, [P, fp, U32, F, F, C.POINTER(MrtHit)]),
+        "mrt_get_counters": (I, [P, C.POINTER(MrtCounters)]),
+        "mrt_reset_counters": (I, [P]),
+        "mrt_scene_device_bytes": (I, [P, C.POINTER(C.c_uint64)]),
+        "mrt_builder_new": (I, [U64, C.POINTER(P)]),
+        "mrt_builder_free": (I, [P]),
+        "mrt_builder_builtin": (I, [P, C.c_char_p, F, C.c_char_p]),
+        "mrt_builder_rand_f32": (F, [P]),
+        "mrt_builder_solid": (I, [P, F, F, F, F]),
+        "mrt_builder_texture_png": (I, [P, C.c_char_p, U32]),
+        "mrt_builder_texture_rgba": (I, [P, C.POINTER(C.c_uint8), U32, U32, U32]),
+        "mrt_builder_material": (I, [P, U32, U32, F, F, F, F]),
+        "mrt_builder_background": (I, [P, U32, U32, F, F, F]),
+        "mrt_builder_add_sphere": (I, [P, U32, F, F, F, F]),
+        "mrt_builder_add_triangle": (I, [P, U32, fp]),
+        "mrt_builder_model": (I, [P, U32, U32, fp, U32, I, I]),
+        "mrt_builder_model_from_ply": (I, [P, C.c_char_p, U32, U32, I]),
+        "mrt_builder_add_instance": (I, [P, I, fp, fp, fp, U32]),
+        "mrt_builder_camera": (I, [P, F, fp, fp, fp, F, F, F]),
+        "mrt_builder_build_bvh": (I, [P]),
+        "mrt_builder_desc": (I, [P, C.POINTER(MrtSceneDesc), C.POINTER(MrtCamera)]),
+        "mrt_load_ply": (I64, [C.c_char_p, fp, U64]),
+        "mrt_load_stl": (I64, [C.c_char_p, fp, U64]),
+        "mrt_load_obj": (I64, [C.c_char_p, fp, U64]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+class MassrtError(RuntimeError):
+    pass
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _f3(v) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(v, dtype=np.float32).reshape(3))
+
+
+def _check_builder(rc: int) -> int:
+    if rc < 0:
+        raise MassrtError(lib().mrt_builder_last_error().decode())
+    return rc
+
+
+class Builder:
+    """Host scene builder (C++ mirror of World/Model/Instance/...)."""
+
+    def __init__(self, rng_seed: int = 1):
+        h = C.c_void_p()
+        if lib().mrt_builder_new(rng_seed, C.byref(h)) != 0:
+            raise MassrtError("mrt_builder_new failed")
+        self.h = h
+        self._keep = []
+
+    def close(self):
+        if self.h:
+            lib().mrt_builder_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def builtin(self, name: str, aspect: float = float(ASPECT_RATIO), asset_dir: str | os.PathLike = ""):
+        rc = lib().mrt_builder_builtin(self.h, name.encode(), aspect, str(asset_dir).encode())
+        if rc != 0:
+            raise MassrtError(lib().mrt_builder_last_error().decode())
+        return self
+
+    def rand_f32(self) -> float:
+        return lib().mrt_builder_rand_f32(self.h)
+
+    def solid(self, r, g, b, a=1.0) -> int:
+        return _check_builder(lib().mrt_builder_solid(self.h, r, g, b, a))
+
+    def texture_rgba(self, rgba: np.ndarray, wrap: int = WRAP_REPEAT) -> int:
+        rgba = np.ascontiguousarray(rgba, dtype=np.uint8)
+        h, w = rgba.shape[:2]
+        return _check_builder(lib().mrt_builder_texture_rgba(self.h, rgba.ctypes.data_as(C.POINTER(C.c_uint8)), w, h, wrap))
+
+    def texture_png(self, path, wrap: int = WRAP_REPEAT) -> int:
+        return _check_builder(lib().mrt_builder_texture_png(self.h, str(path).encode(), wrap))
+
+    def material(self, kind, surface=0, param=0.0, emit=(0.0, 0.0, 0.0)) -> int:
+        return _check_builder(lib().mrt_builder_material(self.h, kind, surface, param, *emit))
+
+    def background(self, kind, surface=0, color=(0.0, 0.0, 0.0)):
+        _check_builder(lib().mrt_builder_background(self.h, kind, surface, *color))
+
+    def add_sphere(self, material, center, radius):
+        _check_builder(lib().mrt_builder_add_sphere(self.h, material, *[float(c) for c in center], radius))
+
+    def add_triangle(self, material, abc):
+        a = np.ascontiguousarray(np.asarray(abc, dtype=np.float32).reshape(9))
+        _check_builder(lib().mrt_builder_add_triangle(self.h, material, _fptr(a)))
+
+    def model(self, tri_material, tris: np.ndarray, override=NO_MATERIAL, add_to_world=False, shading=False) -> int:
+        t = np.ascontiguousarray(tris, dtype=np.float32)
+        n = t.shape[0]
+        return _check_builder(lib().mrt_builder_model(self.h, tri_material, override, _fptr(t), n, int(shading),
+                                                      int(add_to_world)))
+
+    def model_from_ply(self, path, tri_material, override=NO_MATERIAL, add_to_world=False) -> int:
+        return _check_builder(lib().mrt_builder_model_from_ply(self.h, str(path).encode(), tri_material, override,
+                                                               int(add_to_world)))
+
+    def add_instance(self, model, translation, rotation, scale, material=NO_MATERIAL):
+        t, r, s = _f3(translation), _f3(rotation), _f3(scale)
+        _check_builder(lib().mrt_builder_add_instance(self.h, model, _fptr(t), _fptr(r), _fptr(s), material))
+
+    def camera(self, vfov, look_from, look_at, view_up=(0, 1, 0), aspect=float(ASPECT_RATIO), aperture=0.0,
+               focus=None):
+        f, a, u = _f3(look_from), _f3(look_at), _f3(view_up)
+        if focus is None:
+            d = (f - a).astype(np.float32)
+            focus = float(np.sqrt(np.float32(d[0] * d[0] + d[1] * d[1]) + np.float32(d[2] * d[2])))
+        _check_builder(lib().mrt_builder_camera(self.h, vfov, _fptr(f), _fptr(a), _fptr(u), aspect, aperture, focus))
+
+    def build_bvh(self):
+        if lib().mrt_builder_build_bvh(self.h) != 0:
+            raise MassrtError(lib().mrt_builder_last_error().decode())
+
+    def desc(self):
+        d, cam = MrtSceneDesc(), MrtCamera()
+        if lib().mrt_builder_desc(self.h, C.byref(d), C.byref(cam)) != 0:
+            raise MassrtError(lib().mrt_builder_last_error().decode())
+        return d, cam
+
+    def desc_only(self) -> MrtSceneDesc:
+        d = MrtSceneDesc()
+        if lib().mrt_builder_desc(self.h, C.byref(d), None) != 0:
+            raise MassrtError(lib().mrt_builder_last_error().decode())
+        return d
+
+
+def preorder(desc: MrtSceneDesc):
+    """Preorder listing of the world tree in the oracle's format:
+    list of (kind, id) with kind 6 = end of node, plus boxes of nodes."""
+    out, boxes = [], []
+
+    def walk(ref):
+        stack = [("ref", ref)]
+        while stack:
+            tag, r = stack.pop()
+            if tag == "end":
+                out.append((6, 0))
+                boxes.append(None)
+                continue
+            k, i = ref_kind(r), ref_index(r)
+            if k == REF_NODE:
+                n = desc.nodes[i]
+                out.append((REF_NODE, 0))
+                boxes.append(tuple(n.min) + tuple(n.max))
+                stack.append(("end", 0))
+                if ref_kind(n.right) != REF_NONE:
+                    stack.append(("ref", n.right))
+                stack.append(("ref", n.left))
+            else:
+                out.append((k, i))
+                boxes.append(None)
+
+    for r in range(desc.n_roots):
+        walk(desc.roots[r])
+    return out, boxes
+
+
+class Context:
+    """One GPU context (mrt_ctx). Raises if no HIP device is present."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        rc = lib().mrt_create(device, C.byref(h))
+        if rc != 0:
+            raise MassrtError(f"mrt_create failed ({rc}): {lib().mrt_global_last_error().decode()}")
+        self.h = h
+
+    def _check(self, rc):
+        if rc != 0:
+            raise MassrtError(lib().mrt_last_error(self.h).decode())
+
+    def close(self):
+        if self.h:
+            lib().mrt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, builder: Builder):
+        d, cam = builder.desc()
+        self._check(lib().mrt_upload_scene(self.h, C.byref(d)))
+        self._check(lib().mrt_set_camera(self.h, C.byref(cam)))
+
+    def upload_desc(self, desc: MrtSceneDesc):
+        self._check(lib().mrt_upload_scene(self.h, C.byref(desc)))
+
+    def set_camera(self, cam: MrtCamera):
+        self._check(lib().mrt_set_camera(self.h, C.byref(cam)))
+
+    def scene_bytes(self) -> int:
+        v = C.c_uint64()
+        self._check(lib().mrt_scene_device_bytes(self.h, C.byref(v)))
+        return int(v.value)
+
+    @staticmethod
+    def args(width, height, spp_begin=0, spp_count=1, seed=1, max_depth=MAX_DEPTH, shard_index=0, shard_count=1,
+             counters=False) -> MrtRenderArgs:
+        return MrtRenderArgs(width, height, spp_begin, spp_count, seed, max_depth, shard_index, shard_count,
+                             RENDER_COUNTERS if counters else 0)
+
+    def render(self, width, height, spp_begin=0, spp_count=1, seed=1, max_depth=MAX_DEPTH, shard_index=0,
+               shard_count=1, counters=False, accum=None):
+        """Returns (rgb float32 [H*W*3], bounces uint32 [H*W]) accumulated in sample order."""
+        if accum is None:
+            rgb = np.zeros(width * height * 3, dtype=np.float32)
+            b = np.zeros(width * height, dtype=np.uint32)
+        else:
+            rgb, b = accum
+        a = self.args(width, height, spp_begin, spp_count, seed, max_depth, shard_index, shard_count, counters)
+        self._check(lib().mrt_render(self.h, C.byref(a), _fptr(rgb), b.ctypes.data_as(C.POINTER(C.c_uint32))))
+        return rgb, b
+
+    def render_device(self, args: MrtRenderArgs, d_rgb: int, d_bounces: int, stream: int | None = None):
+        self._check(lib().mrt_render_device(self.h, C.byref(args), C.c_void_p(d_rgb), C.c_void_p(d_bounces),
+                                            C.c_void_p(stream or 0)))
+
+    def trace_rays(self, rays: np.ndarray, t_min=0.001, t_max=float("inf")):
+        r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+        n = r.shape[0]
+        out = (MrtHit * max(n, 1))()
+        self._check(lib().mrt_trace_rays(self.h, _fptr(r), n, t_min, t_max, out))
+        a = np.frombuffer(out, dtype=np.uint32).reshape(-1, 4)[:n].copy()
+        return a  # columns: prim, container, t bits, front_face
+
+    def counters(self) -> dict:
+        c = MrtCounters()
+        self._check(lib().mrt_get_counters(self.h, C.byref(c)))
+        return c.as_dict()
+
+    def reset_counters(self):
+        self._check(lib().mrt_reset_counters(self.h))
+
+
+def load_ply(path) -> np.ndarray:
+    n = lib().mrt_load_ply(str(path).encode(), None, 0)
+    if n < 0:
+        raise MassrtError(lib().mrt_builder_last_error().decode())
+    out = np.zeros((n, 9), dtype=np.float32)
+    lib().mrt_load_ply(str(path).encode(), _fptr(out), n)
+    return out
+
+
+def load_stl(path) -> np.ndarray:
+    n = lib().mrt_load_stl(str(path).encode(), None, 0)
+    if n < 0:
+        raise MassrtError(lib().mrt_builder_last_error().decode())
+    out = np.zeros((n, 9), dtype=np.float32)
+    lib().mrt_load_stl(str(path).encode(), _fptr(out), n)
+    return out
+
+
+def load_obj(path) -> np.ndarray:
+    n = lib().mrt_load_obj(str(path).encode(), None, 0)
+    if n < 0:
+        raise MassrtError(lib().mrt_builder_last_error().decode())
+    out = np.zeros((n, 24), dtype=np.float32)
+    lib().mrt_load_obj(str(path).encode(), _fptr(out), n)
+    return out

@@ -1,0 +1,232 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the CPU restatement
+(oracle/oracle.cpp). Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this module; the product never does.
+
+PARITY UNPINNED against the reference binary itself (no Rust toolchain here,
+no golden vectors in the reference); pinned by cube.ply, analytic known
+answers and the published fastrand algorithm. See oracle/oracle.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "_build" / "liboracle.so"
+NO_MATERIAL = 0xFFFFFFFF
+_lib = None
+
+
+def build() -> Path:
+    subprocess.run(["make", "-C", str(HERE), "-s"], check=True)
+    return LIB
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB.exists():
+        build()
+    L = C.CDLL(str(LIB))
+    P, U32, U64, F, I, I64 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_float, C.c_int, C.c_int64
+    fp, up = C.POINTER(C.c_float), C.POINTER(C.c_uint32)
+    sig = {
+        "orc_last_error": (C.c_char_p, []),
+        "orc_new": (P, [U64]),
+        "orc_free": (None, [P]),
+        "orc_builtin": (I, [P, C.c_char_p, F, C.c_char_p]),
+        "orc_rand_f32": (F, [P]),
+        "orc_solid": (I, [P, F, F, F, F]),
+        "orc_texture_rgba": (I, [P, C.POINTER(C.c_uint8), U32, U32, U32]),
+        "orc_texture_png": (I, [P, C.c_char_p, U32]),
+        "orc_material": (I, [P, U32, U32, F, F, F, F]),
+        "orc_background": (I, [P, U32, U32, F, F, F]),
+        "orc_add_sphere": (I, [P, U32, F, F, F, F]),
+        "orc_add_triangle": (I, [P, U32, fp]),
+        "orc_model": (I, [P, U32, U32, fp, U32, I, I]),
+        "orc_model_from_ply": (I, [P, C.c_char_p, U32, U32, I]),
+        "orc_add_instance": (I, [P, I, fp, fp, fp, U32]),
+        "orc_camera": (I, [P, F, fp, fp, fp, F, F, F]),
+        "orc_build_bvh": (I, [P]),
+        "orc_camera_fields": (I, [P, fp]),
+        "orc_export_preorder": (I64, [P, up, fp, U64]),
+        "orc_blas_count": (I64, [P]),
+        "orc_export_blas": (I64, [P, I64, up, fp, U64]),
+        "orc_trace_rays": (I, [P, fp, U32, F, F, P]),
+        "orc_render": (I, [P, U32, U32, U32, U32, U64, U32, U32, U32, I, fp, up]),
+        "orc_render_pixels": (I, [P, U32, U32, up, U32, U32, U32, U64, U32, I, fp, up]),
+        "orc_bench_reference_mode": (C.c_double, [P, U32, U32, U32, U64, U32, I, fp, up, U32, U32]),
+        "orc_get_counters": (None, [P, P]),
+        "orc_reset_counters": (None, [P]),
+        "orc_set_counting": (None, [P, I]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+COUNTER_FIELDS = ["samples", "segments", "node_visits", "sphere_tests", "triangle_tests", "instance_entries",
+                  "model_entries", "closest_hits", "texel_taps", "bounces", "alpha_taps"]
+
+
+class _Counters(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in COUNTER_FIELDS]
+
+
+def _fp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _up(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+def _f3(v):
+    return np.ascontiguousarray(np.asarray(v, dtype=np.float32).reshape(3))
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+class Scene:
+    """Reference-shaped CPU scene (World + Camera) with the builder API of massrt.Builder."""
+
+    def __init__(self, rng_seed: int = 1):
+        self.h = lib().orc_new(rng_seed)
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().orc_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        if rc < 0:
+            raise OracleError(lib().orc_last_error().decode())
+        return rc
+
+    def builtin(self, name, aspect, asset_dir=""):
+        self._chk(lib().orc_builtin(self.h, name.encode(), aspect, str(asset_dir).encode()))
+        return self
+
+    def rand_f32(self):
+        return lib().orc_rand_f32(self.h)
+
+    def solid(self, r, g, b, a=1.0):
+        return self._chk(lib().orc_solid(self.h, r, g, b, a))
+
+    def texture_rgba(self, rgba, wrap=1):
+        rgba = np.ascontiguousarray(rgba, dtype=np.uint8)
+        h, w = rgba.shape[:2]
+        return self._chk(lib().orc_texture_rgba(self.h, rgba.ctypes.data_as(C.POINTER(C.c_uint8)), w, h, wrap))
+
+    def material(self, kind, surface=0, param=0.0, emit=(0.0, 0.0, 0.0)):
+        return self._chk(lib().orc_material(self.h, kind, surface, param, *emit))
+
+    def background(self, kind, surface=0, color=(0.0, 0.0, 0.0)):
+        self._chk(lib().orc_background(self.h, kind, surface, *color))
+
+    def add_sphere(self, material, center, radius):
+        self._chk(lib().orc_add_sphere(self.h, material, *[float(c) for c in center], radius))
+
+    def add_triangle(self, material, abc):
+        a = np.ascontiguousarray(np.asarray(abc, dtype=np.float32).reshape(9))
+        self._chk(lib().orc_add_triangle(self.h, material, _fp(a)))
+
+    def model(self, tri_material, tris, override=NO_MATERIAL, add_to_world=False, shading=False):
+        t = np.ascontiguousarray(tris, dtype=np.float32)
+        return self._chk(lib().orc_model(self.h, tri_material, override, _fp(t), t.shape[0], int(shading),
+                                         int(add_to_world)))
+
+    def model_from_ply(self, path, tri_material, override=NO_MATERIAL, add_to_world=False):
+        return self._chk(lib().orc_model_from_ply(self.h, str(path).encode(), tri_material, override,
+                                                  int(add_to_world)))
+
+    def add_instance(self, model, translation, rotation, scale, material=NO_MATERIAL):
+        t, r, s = _f3(translation), _f3(rotation), _f3(scale)
+        self._chk(lib().orc_add_instance(self.h, model, _fp(t), _fp(r), _fp(s), material))
+
+    def camera(self, vfov, look_from, look_at, view_up=(0, 1, 0), aspect=16 / 9, aperture=0.0, focus=None):
+        f, a, u = _f3(look_from), _f3(look_at), _f3(view_up)
+        if focus is None:
+            d = (f - a).astype(np.float32)
+            focus = float(np.sqrt(np.float32(d[0] * d[0] + d[1] * d[1]) + np.float32(d[2] * d[2])))
+        lib().orc_camera(self.h, vfov, _fp(f), _fp(a), _fp(u), aspect, aperture, focus)
+
+    def build_bvh(self):
+        self._chk(lib().orc_build_bvh(self.h))
+
+    def camera_fields(self) -> np.ndarray:
+        o = np.zeros(19, dtype=np.float32)
+        lib().orc_camera_fields(self.h, _fp(o))
+        return o
+
+    def _listing(self, n, fill):
+        kinds = np.zeros((max(n, 1), 2), dtype=np.uint32)
+        boxes = np.zeros((max(n, 1), 6), dtype=np.float32)
+        fill(_up(kinds), _fp(boxes), n)
+        return kinds[:n], boxes[:n]
+
+    def preorder(self):
+        n = lib().orc_export_preorder(self.h, None, None, 0)
+        return self._listing(n, lambda k, b, c: lib().orc_export_preorder(self.h, k, b, c))
+
+    def blas_count(self):
+        return lib().orc_blas_count(self.h)
+
+    def blas_preorder(self, i):
+        n = lib().orc_export_blas(self.h, i, None, None, 0)
+        return self._listing(n, lambda k, b, c: lib().orc_export_blas(self.h, i, k, b, c))
+
+    def trace_rays(self, rays, t_min=0.001, t_max=float("inf")):
+        r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+        out = np.zeros((r.shape[0], 4), dtype=np.uint32)
+        self._chk(lib().orc_trace_rays(self.h, _fp(r), r.shape[0], t_min, t_max, out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def render(self, width, height, spp_begin=0, spp_count=1, seed=1, max_depth=50, shard_index=0, shard_count=1,
+               threads=0, accum=None):
+        if accum is None:
+            rgb = np.zeros(width * height * 3, dtype=np.float32)
+            b = np.zeros(width * height, dtype=np.uint32)
+        else:
+            rgb, b = accum
+        self._chk(lib().orc_render(self.h, width, height, spp_begin, spp_count, seed, max_depth, shard_index,
+                                   shard_count, threads, _fp(rgb), _up(b)))
+        return rgb, b
+
+    def render_pixels(self, width, height, pixels, spp_begin=0, spp_count=1, seed=1, max_depth=50, threads=0):
+        px = np.ascontiguousarray(pixels, dtype=np.uint32)
+        rgb = np.zeros(px.size * 3, dtype=np.float32)
+        b = np.zeros(px.size, dtype=np.uint32)
+        self._chk(lib().orc_render_pixels(self.h, width, height, _up(px), px.size, spp_begin, spp_count, seed,
+                                          max_depth, threads, _fp(rgb), _up(b)))
+        return rgb, b
+
+    def bench_reference_mode(self, width, height, passes_per_thread, seed=1, max_depth=50, threads=0, row_begin=0,
+                             row_end=0):
+        rgb = np.zeros(width * height * 3, dtype=np.float32)
+        b = np.zeros(width * height, dtype=np.uint32)
+        secs = lib().orc_bench_reference_mode(self.h, width, height, passes_per_thread, seed, max_depth, threads,
+                                              _fp(rgb), _up(b), row_begin, row_end)
+        if secs < 0:
+            raise OracleError("reference-mode bench failed")
+        return secs, rgb, b
+
+    def counters(self) -> dict:
+        c = _Counters()
+        lib().orc_get_counters(self.h, C.byref(c))
+        return {f: int(getattr(c, f)) for f in COUNTER_FIELDS}
+
+    def reset_counters(self):
+        lib().orc_reset_counters(self.h)

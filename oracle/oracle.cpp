@@ -1,0 +1,1524 @@
+// oracle.cpp — TEST INFRASTRUCTURE ONLY (see oracle.h). A CPU restatement of
+// /root/reference/src written in the reference's own shape: objects behind a
+// virtual Intersect, recursive BvhNode/Camera::trace, per-object materials.
+// Every function cites the reference file:line it restates.
+#include "oracle.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <chrono>
+#include <fstream>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace orc {
+
+// ---------------------------------------------------------------- math.rs
+struct V2 {
+  float x, y;
+};
+struct V3 {
+  float x, y, z;
+};
+struct V4 {
+  float x, y, z, w;
+};
+static inline V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+static inline V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static inline V3 operator*(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+static inline V3 operator/(V3 a, V3 b) { return {a.x / b.x, a.y / b.y, a.z / b.z}; }
+static inline V3 operator*(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+static inline V3 operator/(V3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+static inline V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
+static inline V2 operator+(V2 a, V2 b) { return {a.x + b.x, a.y + b.y}; }
+static inline V2 operator-(V2 a, V2 b) { return {a.x - b.x, a.y - b.y}; }
+static inline V2 operator*(V2 a, float s) { return {a.x * s, a.y * s}; }
+static inline V4 operator+(V4 a, V4 b) { return {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
+static inline V4 operator*(V4 a, float s) { return {a.x * s, a.y * s, a.z * s, a.w * s}; }
+static inline V3 fill(float f) { return {f, f, f}; }
+// generic.rs:8-18
+static inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline V3 cross(V3 a, V3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+// generic.rs:20-34 (f32::min/max ignore NaN)
+static inline V3 vmin(V3 a, V3 b) { return {fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z)}; }
+static inline V3 vmax(V3 a, V3 b) { return {fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z)}; }
+// math.rs:250-260
+static inline float length_squared(V3 a) { return dot(a, a); }
+static inline float length(V3 a) { return sqrtf(length_squared(a)); }
+static inline V3 unit(V3 a) { return a / length(a); }
+// math.rs:293-306
+static inline bool near_zero(V3 a) { return fabsf(a.x) <= 0.00001f && fabsf(a.y) <= 0.00001f && fabsf(a.z) <= 0.00001f; }
+static inline V3 reflect(V3 v, V3 n) { return v - ((n * dot(v, n)) * 2.0f); }
+static inline V3 refract(V3 v, V3 n, float eta) {
+  float cos_theta = fminf(dot(-v, n), 1.0f);
+  V3 perp = (v + n * cos_theta) * eta;
+  V3 par = n * (-sqrtf(fabsf(1.0f - length_squared(perp))));
+  return perp + par;
+}
+
+// generic.rs:71-159 column-major M4
+struct M4 {
+  V4 c[4];
+};
+static inline float dot4(V4 a, V4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
+static M4 transpose(const M4& m) {
+  M4 t;
+  t.c[0] = {m.c[0].x, m.c[1].x, m.c[2].x, m.c[3].x};
+  t.c[1] = {m.c[0].y, m.c[1].y, m.c[2].y, m.c[3].y};
+  t.c[2] = {m.c[0].z, m.c[1].z, m.c[2].z, m.c[3].z};
+  t.c[3] = {m.c[0].w, m.c[1].w, m.c[2].w, m.c[3].w};
+  return t;
+}
+static M4 mul(const M4& a, const M4& b) {
+  M4 m = transpose(a), r;
+  for (int j = 0; j < 4; ++j)
+    r.c[j] = {dot4(m.c[0], b.c[j]), dot4(m.c[1], b.c[j]), dot4(m.c[2], b.c[j]), dot4(m.c[3], b.c[j])};
+  return r;
+}
+static V3 transform(const M4& m, V3 p, float w) {
+  V4 vx = m.c[0] * p.x, vy = m.c[1] * p.y, vz = m.c[2] * p.z, vw = m.c[3] * w;
+  V4 v = ((vx + vy) + vz) + vw;
+  return {v.x, v.y, v.z};
+}
+static const float PI = 3.14159265358979323846f;
+__attribute__((noinline)) static float o_sin(float x) { return sinf(x); }
+__attribute__((noinline)) static float o_cos(float x) { return cosf(x); }
+__attribute__((noinline)) static float o_tan(float x) { return tanf(x); }
+// math.rs:357-406
+static M4 mk(V4 a, V4 b, V4 c, V4 d) {
+  M4 m;
+  m.c[0] = a, m.c[1] = b, m.c[2] = c, m.c[3] = d;
+  return m;
+}
+static M4 translation(V3 t) { return mk({1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {t.x, t.y, t.z, 1}); }
+static M4 rotate_x(float a) {
+  float r = a * PI * 2.0f, s = o_sin(r), c = o_cos(r);
+  return mk({1, 0, 0, 0}, {0, c, s, 0}, {0, -s, c, 0}, {0, 0, 0, 1});
+}
+static M4 rotate_y(float a) {
+  float r = a * PI * 2.0f, s = o_sin(r), c = o_cos(r);
+  return mk({c, 0, s, 0}, {0, 1, 0, 0}, {-s, 0, c, 0}, {0, 0, 0, 1});
+}
+static M4 rotate_z(float a) {
+  float r = a * PI * 2.0f, s = o_sin(r), c = o_cos(r);
+  return mk({c, -s, 0, 0}, {s, c, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1});
+}
+static M4 scale_m(V3 s) { return mk({s.x, 0, 0, 0}, {0, s.y, 0, 0}, {0, 0, s.z, 0}, {0, 0, 0, 1}); }
+
+// ---------------------------------------------------------------- RNG
+// fastrand 1.4.1 wyrand (Cargo.lock:579-582), as published.
+struct Wy {
+  uint64_t s;
+  uint64_t u64() {
+    s += 0xA0761D6478BD642FULL;
+    unsigned __int128 t = (unsigned __int128)s * (unsigned __int128)(s ^ 0xE7037ED1A0B428DBULL);
+    return (uint64_t)(t >> 64) ^ (uint64_t)t;
+  }
+  uint32_t u32() { return (uint32_t)u64(); }
+  float f32() {
+    uint32_t b = 0x3F800000u | (u32() >> 9);
+    float f;
+    memcpy(&f, &b, 4);
+    return f - 1.0f;
+  }
+  uint32_t mod(uint32_t n) {  // Lemire, fastrand gen_mod_u32
+    uint32_t r = u32();
+    uint64_t m = (uint64_t)r * n;
+    if ((uint32_t)m < n) {
+      uint32_t t = (uint32_t)(-n) % n;
+      while ((uint32_t)m < t) m = (uint64_t)u32() * n;
+    }
+    return (uint32_t)(m >> 32);
+  }
+};
+// Per-(pixel, sample) stream shared with the GPU: splitmix64 -> xoroshiro128**
+static uint64_t sm64(uint64_t& x) {
+  uint64_t z = (x += 0x9E3779B97F4A7C15ULL);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+struct PathRng {
+  uint64_t a, b;
+  PathRng(uint64_t seed, uint32_t pixel, uint32_t sample) {
+    uint64_t x = seed;
+    uint64_t k = sm64(x);
+    x = k ^ (((uint64_t)pixel << 32) | sample);
+    a = sm64(x);
+    b = sm64(x);
+    if ((a | b) == 0) b = 1;
+  }
+  static uint64_t rotl(uint64_t v, int k) { return (v << k) | (v >> (64 - k)); }
+  uint64_t next() {
+    uint64_t s0 = a, s1 = b, r = rotl(s0 * 5, 7) * 9;
+    s1 ^= s0;
+    a = rotl(s0, 24) ^ s1 ^ (s1 << 16);
+    b = rotl(s1, 37);
+    return r;
+  }
+  float f32() {  // Num::rand mapping (math.rs:244-246 -> fastrand::f32)
+    uint32_t bits = 0x3F800000u | ((uint32_t)(next() >> 32) >> 9);
+    float f;
+    memcpy(&f, &bits, 4);
+    return f - 1.0f;
+  }
+};
+
+struct Counters {
+  uint64_t samples = 0, segments = 0, node_visits = 0, sphere_tests = 0, triangle_tests = 0, instance_entries = 0,
+           model_entries = 0, closest_hits = 0, texel_taps = 0, bounces = 0, alpha_taps = 0;
+  void add(const Counters& o) {
+    samples += o.samples, segments += o.segments, node_visits += o.node_visits, sphere_tests += o.sphere_tests;
+    triangle_tests += o.triangle_tests, instance_entries += o.instance_entries, model_entries += o.model_entries;
+    closest_hits += o.closest_hits, texel_taps += o.texel_taps, bounces += o.bounces, alpha_taps += o.alpha_taps;
+  }
+};
+struct Ctx {
+  PathRng* rng = nullptr;
+  Counters cnt;
+  bool in_alpha = false;
+  float rand() { return rng->f32(); }
+};
+
+// math.rs:262-287
+static V3 random_in_unit_sphere(Ctx& c) {
+  for (;;) {
+    float x = c.rand() * 2.0f - 1.0f;
+    float y = c.rand() * 2.0f - 1.0f;
+    float z = c.rand() * 2.0f - 1.0f;
+    V3 v{x, y, z};
+    if (length_squared(v) >= 1.0f) continue;
+    return v;
+  }
+}
+static V3 random_in_unit_disk(Ctx& c) {
+  for (;;) {
+    float x = c.rand() * 2.0f - 1.0f;
+    float y = c.rand() * 2.0f - 1.0f;
+    V3 v{x, y, 0.0f};
+    if (length_squared(v) >= 1.0f) continue;
+    return v;
+  }
+}
+
+// ---------------------------------------------------------------- world.rs:168-182
+struct Ray {
+  V3 origin, direction;
+  V3 at(float t) const { return origin + (direction * t); }
+};
+
+// ---------------------------------------------------------------- texture.rs
+struct Surface {
+  virtual ~Surface() {}
+  virtual V4 get_f(V2 index, Ctx& c) const = 0;
+};
+struct SolidColor : Surface {  // texture.rs:179-194
+  V4 c;
+  explicit SolidColor(V4 v) : c(v) {}
+  V4 get_f(V2, Ctx&) const override { return c; }
+};
+enum { WRAP_MIRROR = 0, WRAP_REPEAT = 1, WRAP_CLAMP = 2 };
+static float fract(float x) { return x - truncf(x); }
+static size_t as_usize(float f) { return f > 0.0f ? (size_t)f : 0; }
+struct Texture : Surface {  // texture.rs:21-149
+  uint32_t w, h, wrap;
+  std::vector<V4> px;
+  Texture(const uint8_t* rgba, uint32_t w_, uint32_t h_, uint32_t wrap_) : w(w_), h(h_), wrap(wrap_) {
+    px.resize((size_t)w * h);
+    for (size_t i = 0; i < px.size(); ++i)
+      px[i] = V4{(float)rgba[4 * i] / 255.0f, (float)rgba[4 * i + 1] / 255.0f, (float)rgba[4 * i + 2] / 255.0f,
+                 (float)rgba[4 * i + 3] / 255.0f};
+  }
+  const V4& at(size_t x, size_t y) const {
+    size_t i = y * w + x;
+    if (i >= px.size()) throw std::runtime_error("texture index out of bounds (reference panics)");
+    return px[i];
+  }
+  V2 wrap_uv(V2 o) const {  // texture.rs:278-299
+    if (wrap == WRAP_MIRROR) throw std::runtime_error("Mirror wrapping is not implemented");
+    if (wrap == WRAP_REPEAT) {
+      float x = o.x, y = o.y;
+      x = x < 0.0f ? 1.0f - fract(fabsf(x)) : x;
+      y = y < 0.0f ? 1.0f - fract(fabsf(y)) : y;
+      x = x > 1.0f ? fract(x) : x;
+      y = y > 1.0f ? fract(y) : y;
+      return {x, y};
+    }
+    return {fmaxf(fminf(o.x, 1.0f), 0.0f), fmaxf(fminf(o.y, 1.0f), 0.0f)};
+  }
+  V4 get_f(V2 index, Ctx& c) const override {
+    if (c.in_alpha)
+      c.cnt.alpha_taps += 4;
+    else
+      c.cnt.texel_taps += 4;
+    V2 i = wrap_uv(index);
+    float x = i.x * (float)(w - 1);
+    float y = i.y * (float)(h - 1);
+    size_t x0 = as_usize(floorf(x)), x1 = as_usize(ceilf(x));
+    size_t y0 = as_usize(floorf(y)), y1 = as_usize(ceilf(y));
+    float t = x - (float)x0;
+    V4 p0 = at(x0, y0) * (1.0f - t) + at(x1, y0) * t;
+    V4 p1 = at(x0, y1) * (1.0f - t) + at(x1, y1) * t;
+    t = y - (float)y0;
+    return p1 * t + p0 * (1.0f - t);
+  }
+};
+
+// ---------------------------------------------------------------- geom.rs Hit
+struct Material;
+struct Hit {  // geom.rs:7-33
+  V3 point, normal;
+  bool has_uv = false;
+  V2 uv{0, 0};
+  float t = 0;
+  bool front_face = false;
+  const Material* material = nullptr;
+  uint32_t prim = 0, container = 0;  // parity ids (not in the reference)
+  void set_face_normal(const Ray& r, V3 outward) {
+    front_face = dot(r.direction, outward) < 0.0f;
+    normal = front_face ? outward : -outward;
+  }
+};
+struct Scatter {
+  V3 attenuation;
+  Ray scattered;
+};
+
+// ---------------------------------------------------------------- material.rs
+struct Material {  // material.rs:15-27
+  virtual ~Material() {}
+  virtual bool scatter(const Ray& ray, const Hit& hit, Ctx& c, Scatter& out) const = 0;
+  virtual bool emit(const Hit&, V3&) const { return false; }
+  virtual bool alpha_test(V2, Ctx&) const { return true; }
+};
+struct NoMaterial : Material {  // material.rs:385-389
+  bool scatter(const Ray&, const Hit&, Ctx&, Scatter&) const override { return false; }
+};
+struct Lambertian : Material {  // material.rs:192-225
+  std::shared_ptr<Surface> surface;
+  explicit Lambertian(std::shared_ptr<Surface> s) : surface(std::move(s)) {}
+  bool scatter(const Ray&, const Hit& hit, Ctx& c, Scatter& out) const override {
+    V3 dir = hit.normal + unit(random_in_unit_sphere(c));
+    if (near_zero(dir)) dir = hit.normal;
+    out.scattered = Ray{hit.point, dir};
+    V4 a = surface->get_f(hit.has_uv ? hit.uv : V2{0, 0}, c);
+    out.attenuation = V3{a.x, a.y, a.z};
+    return true;
+  }
+  bool alpha_test(V2 uv, Ctx& c) const override {
+    c.in_alpha = true;
+    bool r = surface->get_f(uv, c).w != 0.0f;
+    c.in_alpha = false;
+    return r;
+  }
+};
+struct Metal : Material {  // material.rs:248-284
+  float fuzz;
+  std::shared_ptr<Surface> surface;
+  Metal(float f, std::shared_ptr<Surface> s) : fuzz(f < 1.0f ? f : 1.0f), surface(std::move(s)) {}
+  bool scatter(const Ray& ray, const Hit& hit, Ctx& c, Scatter& out) const override {
+    V3 reflected = reflect(unit(ray.direction), hit.normal);
+    Ray sc{hit.point, reflected + (random_in_unit_sphere(c) * fuzz)};
+    if (dot(sc.direction, hit.normal) > 0.0f) {
+      V4 a = surface->get_f(hit.has_uv ? hit.uv : V2{0, 0}, c);
+      out.attenuation = V3{a.x, a.y, a.z};
+      out.scattered = sc;
+      return true;
+    }
+    return false;
+  }
+  bool alpha_test(V2 uv, Ctx& c) const override {
+    c.in_alpha = true;
+    bool r = surface->get_f(uv, c).w != 0.0f;
+    c.in_alpha = false;
+    return r;
+  }
+};
+struct Dielectric : Material {  // material.rs:286-329
+  float ior;
+  explicit Dielectric(float i) : ior(i) {}
+  static float reflectance(float cosine, float ref_idx) {
+    float r0 = (1.0f - ref_idx) / (1.0f + ref_idx);
+    r0 = r0 * r0;  // powi(2)
+    float x = 1.0f - cosine;
+    return r0 + (1.0f - r0) * (x * ((x * x) * (x * x)));  // powi(5) (LLVM ExpandPowI)
+  }
+  bool scatter(const Ray& ray, const Hit& hit, Ctx& c, Scatter& out) const override {
+    float ratio = hit.front_face ? 1.0f / ior : ior;
+    V3 ud = unit(ray.direction);
+    float cos_theta = fminf(dot(-ud, hit.normal), 1.0f);
+    float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
+    bool cannot = ratio * sin_theta > 1.0f;
+    V3 dir;
+    if (cannot || reflectance(cos_theta, ratio) > c.rand())
+      dir = reflect(ud, hit.normal);
+    else
+      dir = refract(ud, hit.normal, ratio);
+    out.attenuation = fill(1.0f);
+    out.scattered = Ray{hit.point, dir};
+    return true;
+  }
+};
+struct DiffuseLight : Material {  // material.rs:227-246
+  V3 e;
+  explicit DiffuseLight(V3 v) : e(v) {}
+  bool scatter(const Ray&, const Hit&, Ctx&, Scatter&) const override { return false; }
+  bool emit(const Hit&, V3& out) const override {
+    out = e;
+    return true;
+  }
+};
+
+struct Background {
+  virtual ~Background() {}
+  virtual V3 background(const Ray& r, Ctx& c) const = 0;
+};
+struct SolidBackground : Background {  // material.rs:39-53
+  V3 color;
+  explicit SolidBackground(V3 c) : color(c) {}
+  V3 background(const Ray&, Ctx&) const override { return color; }
+};
+struct SkyBackground : Background {  // material.rs:55-63
+  V3 background(const Ray& r, Ctx&) const override {
+    V3 u = unit(r.direction);
+    float t = 0.5f * (u.y + 1.0f);
+    return (fill(1.0f) * (1.0f - t)) + (V3{0.5f, 0.7f, 1.0f} * t);
+  }
+};
+struct SkySphere : Background {  // material.rs:65-89
+  std::shared_ptr<Surface> tex;
+  explicit SkySphere(std::shared_ptr<Surface> t) : tex(std::move(t)) {}
+  V3 background(const Ray& r, Ctx& c) const override {
+    V3 p = unit(r.direction);
+    float theta = acosf(p.y);
+    float phi = atan2f(p.z * -1.0f, p.x) + PI;
+    V4 px = tex->get_f(V2{phi / (2.0f * PI), theta / PI}, c);
+    return V3{px.x, px.y, px.z};
+  }
+};
+
+// ---------------------------------------------------------------- geom.rs
+enum { REF_NONE = 0, REF_NODE = 1, REF_SPHERE = 2, REF_TRI = 3, REF_INST = 4, REF_MODEL = 5 };
+static inline uint32_t mkref(uint32_t k, uint32_t i) { return (k << 28) | i; }
+
+struct BoundingBox {  // geom.rs:207-273
+  V3 minimum, maximum;
+  bool hit(const Ray& ray, float t_min, float t_max, Ctx& c) const {
+    c.cnt.node_visits++;
+    V3 v_min = (minimum - ray.origin) / ray.direction;
+    V3 v_max = (maximum - ray.origin) / ray.direction;
+    V3 mn = vmin(v_min, v_max), mx = vmax(v_min, v_max);
+    float lo = fmaxf(mn.x, t_min), hi = fminf(mx.x, t_max);
+    if (hi < lo) return false;
+    lo = fmaxf(mn.y, lo), hi = fminf(mx.y, hi);
+    if (hi < lo) return false;
+    lo = fmaxf(mn.z, lo), hi = fminf(mx.z, hi);
+    if (hi < lo) return false;
+    return true;
+  }
+  BoundingBox join(const BoundingBox& o) const { return {vmin(minimum, o.minimum), vmax(maximum, o.maximum)}; }
+  V3 corner(int i) const {
+    return {(i & 1) == 0 ? maximum.x : minimum.x, (i & 2) == 0 ? maximum.y : minimum.y,
+            (i & 4) == 0 ? maximum.z : minimum.z};
+  }
+};
+
+struct PreorderSink {
+  std::vector<uint32_t> kinds;  // pairs kind, id
+  std::vector<float> boxes;     // 6 per element
+  void push(uint32_t k, uint32_t id, const BoundingBox* b) {
+    kinds.push_back(k), kinds.push_back(id);
+    if (b) {
+      const float v[6] = {b->minimum.x, b->minimum.y, b->minimum.z, b->maximum.x, b->maximum.y, b->maximum.z};
+      boxes.insert(boxes.end(), v, v + 6);
+    } else {
+      boxes.insert(boxes.end(), 6, 0.0f);
+    }
+  }
+};
+
+struct Intersect {  // geom.rs:35-38
+  virtual ~Intersect() {}
+  virtual bool intersect(const Ray& ray, float t_min, float t_max, Hit& out, Ctx& c) const = 0;
+  virtual BoundingBox bounding_box() const = 0;
+  virtual void preorder(PreorderSink& s) const = 0;
+};
+using Obj = std::unique_ptr<Intersect>;
+
+struct Sphere : Intersect {  // geom.rs:40-101
+  V3 center;
+  float radius;
+  std::shared_ptr<Material> material;
+  uint32_t id;
+  bool intersect(const Ray& ray, float t_min, float t_max, Hit& out, Ctx& c) const override {
+    c.cnt.sphere_tests++;
+    V3 oc = ray.origin - center;
+    float a = length_squared(ray.direction);
+    float half_b = dot(oc, ray.direction);
+    float cc = length_squared(oc) - (radius * radius);
+    float disc = (half_b * half_b) - (a * cc);
+    if (disc < 0.0f) return false;
+    float sq = sqrtf(disc);
+    float root = (-half_b - sq) / a;
+    if (root < t_min || t_max < root) {
+      root = (-half_b + sq) / a;
+      if (root < t_min || t_max < root) return false;
+    }
+    Hit h;
+    h.point = ray.at(root);
+    V3 n = (h.point - center) / radius;
+    h.t = root;
+    h.has_uv = false;
+    h.material = material.get();
+    h.set_face_normal(ray, n);
+    h.prim = mkref(REF_SPHERE, id);
+    out = h;
+    return true;
+  }
+  BoundingBox bounding_box() const override {
+    float r = fabsf(radius);
+    return {center - fill(r), center + fill(r)};
+  }
+  void preorder(PreorderSink& s) const override { s.push(REF_SPHERE, id, nullptr); }
+};
+
+struct Triangle : Intersect {  // geom.rs:427-593
+  V3 a, b, c;
+  bool has_uv = false;
+  V2 uva{0, 0}, uvb{0, 0}, uvc{0, 0};
+  std::shared_ptr<Material> material;
+  V3 na, nb, nc, tangent{0, 0, 0}, bitangent{0, 0, 0};
+  uint32_t id = 0;
+  bool intersect(const Ray& ray, float t_min, float t_max, Hit& out, Ctx& cx) const override {
+    cx.cnt.triangle_tests++;
+    V3 ab = b - a, ac = c - a;
+    V3 p_vec = cross(ray.direction, ac);
+    float det = dot(ab, p_vec);
+    if (fabsf(det) < 0.000001f) return false;
+    float inv_det = 1.0f / det;
+    V3 t_vec = ray.origin - a;
+    float u = dot(t_vec, p_vec) * inv_det;
+    if (u < 0.0f || u > 1.0f) return false;
+    V3 q_vec = cross(t_vec, ab);
+    float v = dot(ray.direction, q_vec) * inv_det;
+    if (v < 0.0f || v + u > 1.0f) return false;
+    float t = dot(ac, q_vec) * inv_det;
+    if (t < t_min || t > t_max) return false;
+    V3 point = ray.at(t);
+    V3 d0 = a - point, d1 = b - point, d2 = c - point;
+    float area = length(cross(a - b, a - c));
+    float a0 = length(cross(d1, d2)) / area;
+    float a1 = length(cross(d2, d0)) / area;
+    float a2 = length(cross(d0, d1)) / area;
+    V3 normal = na * a0 + nb * a1 + nc * a2;
+    Hit h;
+    if (has_uv) {
+      V2 uv = uva * a0 + uvb * a1 + uvc * a2;
+      // material.normal(uv) is None for every in-scope material (material.rs:20-22)
+      h.has_uv = true;
+      h.uv = uv;
+      if (!material->alpha_test(uv, cx)) return false;
+    }
+    h.point = point;
+    h.t = t;
+    h.material = material.get();
+    h.set_face_normal(ray, normal);
+    h.prim = mkref(REF_TRI, id);
+    out = h;
+    return true;
+  }
+  BoundingBox bounding_box() const override { return {vmin(vmin(a, b), c), vmax(vmax(a, b), c)}; }
+  void preorder(PreorderSink& s) const override { s.push(REF_TRI, id, nullptr); }
+};
+
+static float cmp_key(const Intersect* o, uint32_t axis) {
+  BoundingBox b = o->bounding_box();
+  return axis == 0 ? b.minimum.x : axis == 1 ? b.minimum.y : b.minimum.z;
+}
+
+struct BvhNode : Intersect {  // geom.rs:103-205
+  Obj left, right;
+  BoundingBox box;
+  BvhNode(std::vector<Obj> items, Wy& rng) {
+    if (items.empty()) throw std::runtime_error("BvhNode::new(empty) recurses forever in the reference");
+    uint32_t axis = rng.mod(3);  // fastrand::u8(0..3)
+    if (items.size() == 1) {
+      left = std::move(items[0]);
+    } else if (items.size() == 2) {
+      Obj a = std::move(items[1]);  // items.pop()
+      Obj b = std::move(items[0]);  // items.pop()
+      if (cmp_key(a.get(), axis) < cmp_key(b.get(), axis)) {
+        left = std::move(a), right = std::move(b);
+      } else {
+        left = std::move(b), right = std::move(a);
+      }
+    } else {
+      std::stable_sort(items.begin(), items.end(),
+                       [axis](const Obj& x, const Obj& y) { return cmp_key(x.get(), axis) < cmp_key(y.get(), axis); });
+      size_t mid = items.size() / 2;
+      std::vector<Obj> back;
+      for (size_t i = mid; i < items.size(); ++i) back.push_back(std::move(items[i]));
+      items.resize(mid);
+      left = Obj(new BvhNode(std::move(items), rng));
+      right = Obj(new BvhNode(std::move(back), rng));
+    }
+    box = right ? left->bounding_box().join(right->bounding_box()) : left->bounding_box();
+  }
+  bool intersect(const Ray& ray, float t_min, float t_max, Hit& out, Ctx& c) const override {
+    if (!box.hit(ray, t_min, t_max, c)) return false;
+    Hit lh;
+    bool l = left && left->intersect(ray, t_min, t_max, lh, c);
+    float tm = l ? lh.t : t_max;
+    Hit rh;
+    if (right && right->intersect(ray, t_min, tm, rh, c)) {
+      out = rh;
+      return true;
+    }
+    if (l) out = lh;
+    return l;
+  }
+  BoundingBox bounding_box() const override { return box; }
+  void preorder(PreorderSink& s) const override {
+    s.push(REF_NODE, 0, &box);
+    left->preorder(s);
+    if (right) right->preorder(s);
+    s.push(6, 0, nullptr);
+  }
+};
+
+struct Model : Intersect {  // geom.rs:275-333
+  std::shared_ptr<BvhNode> tris;
+  std::shared_ptr<Material> material;  // override or null
+  uint32_t id = 0;
+  bool intersect(const Ray& ray, float t_min, float t_max, Hit& out, Ctx& c) const override {
+    c.cnt.model_entries++;
+    if (!tris->intersect(ray, t_min, t_max, out, c)) return false;
+    if (material) out.material = material.get();
+    out.container = mkref(REF_MODEL, id);
+    return true;
+  }
+  BoundingBox bounding_box() const override { return tris->bounding_box(); }
+  void preorder(PreorderSink& s) const override { s.push(REF_MODEL, id, nullptr); }
+};
+
+struct Instance : Intersect {  // geom.rs:335-425
+  std::shared_ptr<BvhNode> tris;
+  std::shared_ptr<Material> material;
+  M4 fwd, inv;
+  BoundingBox box;
+  uint32_t id = 0;
+  Instance(std::shared_ptr<BvhNode> t, V3 tr, V3 rot, V3 sc) : tris(std::move(t)) {
+    V3 itr = tr * -1.0f, irot = rot * -1.0f;
+    V3 isc{1.0f / sc.x, 1.0f / sc.y, 1.0f / sc.z};
+    M4 T = translation(tr), IT = translation(itr);
+    M4 R = mul(mul(rotate_x(rot.x), rotate_y(rot.y)), rotate_z(rot.z));
+    M4 IR = mul(mul(rotate_z(irot.z), rotate_y(irot.y)), rotate_x(irot.x));
+    fwd = mul(mul(T, R), scale_m(sc));
+    inv = mul(mul(scale_m(isc), IR), IT);
+    V3 mn = fill(INFINITY), mx = fill(-INFINITY);
+    BoundingBox tb = tris->bounding_box();
+    for (int i = 0; i < 8; ++i) {
+      V3 p = transform(fwd, tb.corner(i), 1.0f);
+      mn = vmin(mn, p);
+      mx = vmax(mx, p);
+    }
+    box = {mn, mx};
+  }
+  bool intersect(const Ray& ray, float t_min, float t_max, Hit& out, Ctx& c) const override {
+    c.cnt.instance_entries++;
+    Ray r{transform(inv, ray.origin, 1.0f), transform(inv, ray.direction, 0.0f)};
+    if (!tris->intersect(r, t_min, t_max, out, c)) return false;
+    out.point = transform(fwd, out.point, 1.0f);
+    out.normal = unit(transform(fwd, out.normal, 0.0f));
+    if (material) out.material = material.get();
+    out.container = mkref(REF_INST, id);
+    return true;
+  }
+  BoundingBox bounding_box() const override { return box; }
+  void preorder(PreorderSink& s) const override { s.push(REF_INST, id, nullptr); }
+};
+
+// ---------------------------------------------------------------- world.rs
+struct Camera {  // world.rs:5-63
+  V3 origin, llc, horizontal, vertical, u, v;
+  float lens_radius = 0;
+  static Camera make(float vfov, V3 from, V3 at, V3 up, float aspect, float aperture, float focus) {
+    float rads = vfov * PI / 180.0f;
+    float half_height = o_tan(rads / 2.0f);
+    float vh = half_height * 2.0f;
+    float vw = aspect * vh;
+    V3 w = unit(from - at);
+    V3 uu = unit(cross(up, w));
+    V3 vv = cross(w, uu);
+    Camera c;
+    c.origin = from;
+    c.horizontal = uu * vw * focus;
+    c.vertical = vv * vh * focus;
+    c.llc = c.origin - (c.horizontal / 2.0f) - (c.vertical / 2.0f) - (w * focus);
+    c.u = uu;
+    c.v = vv;
+    c.lens_radius = aperture / 2.0f;
+    return c;
+  }
+  Ray ray(float s, float t, Ctx& c) const {
+    V3 blur = random_in_unit_disk(c) * lens_radius;
+    V3 offset = u * blur.x + v * blur.y;
+    return Ray{origin + offset, llc + (horizontal * s) + (vertical * t) - origin - offset};
+  }
+};
+
+struct World {  // world.rs:95-166
+  std::unique_ptr<Background> background = std::unique_ptr<Background>(new SolidBackground(V3{0, 0, 0}));
+  std::vector<Obj> objects;
+  bool intersect(const Ray& ray, float t_min, float t_max, Hit& out, Ctx& c) const {
+    c.cnt.segments++;
+    bool found = false;
+    float closest = t_max;
+    for (const Obj& o : objects) {
+      Hit h;
+      if (o->intersect(ray, t_min, closest, h, c)) {
+        closest = h.t;
+        out = h;
+        found = true;
+      }
+    }
+    if (found) c.cnt.closest_hits++;
+    return found;
+  }
+};
+
+// Camera::trace (world.rs:65-79): recursive, post-order radiance fold
+static std::pair<V3, uint32_t> trace(const World& w, const Ray& ray, uint32_t depth, Ctx& c) {
+  if (depth == 0) return {fill(0.0f), depth};
+  Hit hit;
+  if (w.intersect(ray, 0.001f, INFINITY, hit, c)) {
+    V3 emitted{0, 0, 0};
+    hit.material->emit(hit, emitted);
+    Scatter s;
+    if (hit.material->scatter(ray, hit, c, s)) {
+      c.cnt.bounces++;
+      auto r = trace(w, s.scattered, depth - 1, c);
+      return {(r.first * s.attenuation) + emitted, r.second};
+    }
+    return {emitted, depth};
+  }
+  return {w.background->background(ray, c), depth};
+}
+
+}  // namespace orc
+
+// =========================================================================
+using namespace orc;
+
+struct orc_scene {
+  Wy rng;
+  World world;
+  Camera camera;
+  std::vector<std::shared_ptr<Surface>> surfaces;
+  std::vector<std::shared_ptr<Material>> materials;
+  std::vector<std::shared_ptr<BvhNode>> blas;  // every Model's BvhNode in creation order
+  std::vector<std::shared_ptr<Material>> model_override;
+  uint32_t n_spheres = 0, n_tris = 0, n_inst = 0, n_models = 0;
+  std::vector<Model*> world_models;  // models added to the world
+  Counters counters;
+  std::mutex mu;
+  bool counting = true;
+};
+
+static thread_local std::string g_err;
+const char* orc_last_error(void) { return g_err.c_str(); }
+
+template <typename F>
+static int guard(F&& f) {
+  try {
+    return f();
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+static V3 v3p(const float* p) { return V3{p[0], p[1], p[2]}; }
+
+// --------------------------------------------------------------- loaders
+namespace {
+// ply_loader.rs:273-430 (triangles only)
+struct PlyIn {
+  FILE* f;
+  explicit PlyIn(const std::string& p) : f(fopen(p.c_str(), "rb")) {
+    if (!f) throw std::runtime_error("cannot open " + p);
+  }
+  ~PlyIn() { fclose(f); }
+  int get() { return fgetc(f); }
+  std::string line() {
+    std::string s;
+    int c;
+    while ((c = get()) != EOF) {
+      s.push_back((char)c);
+      if (c == '\n') break;
+    }
+    return s;
+  }
+  std::string word() {
+    std::string w;
+    for (;;) {
+      int c = get();
+      if (c == EOF) throw std::runtime_error("ply eof");
+      if (isspace(c)) {
+        if (!w.empty()) return w;
+      } else {
+        w.push_back((char)c);
+      }
+    }
+  }
+  void bytes(void* d, size_t n) {
+    if (fread(d, 1, n, f) != n) throw std::runtime_error("ply eof");
+  }
+};
+int ply_size(const std::string& t) {
+  if (t == "char" || t == "int8" || t == "uchar" || t == "uint8") return 1;
+  if (t == "short" || t == "int16" || t == "ushort" || t == "uint16") return 2;
+  if (t == "int" || t == "int32" || t == "uint" || t == "uint32" || t == "float" || t == "float32") return 4;
+  if (t == "double" || t == "float64") return 8;
+  return 0;
+}
+double ply_bin(PlyIn& in, const std::string& t, bool be) {
+  unsigned char b[8];
+  int n = ply_size(t);
+  in.bytes(b, n);
+  if (be) std::reverse(b, b + n);
+  if (t == "char" || t == "int8") return (int8_t)b[0];
+  if (t == "uchar" || t == "uint8") return b[0];
+  int16_t i16;
+  uint16_t u16;
+  int32_t i32;
+  uint32_t u32;
+  float f;
+  double d;
+  if (t == "short" || t == "int16") return memcpy(&i16, b, 2), i16;
+  if (t == "ushort" || t == "uint16") return memcpy(&u16, b, 2), u16;
+  if (t == "int" || t == "int32") return memcpy(&i32, b, 4), i32;
+  if (t == "uint" || t == "uint32") return memcpy(&u32, b, 4), u32;
+  if (t == "float" || t == "float32") return memcpy(&f, b, 4), f;
+  return memcpy(&d, b, 8), d;
+}
+std::vector<std::string> split1(const std::string& s) {
+  std::vector<std::string> out;
+  size_t st = 0;
+  for (;;) {
+    size_t p = s.find(' ', st);
+    out.push_back(s.substr(st, p == std::string::npos ? std::string::npos : p - st));
+    if (p == std::string::npos) return out;
+    st = p + 1;
+  }
+}
+std::string trimmed(std::string s) {
+  while (!s.empty() && isspace((unsigned char)s.back())) s.pop_back();
+  size_t a = 0;
+  while (a < s.size() && isspace((unsigned char)s[a])) ++a;
+  return s.substr(a);
+}
+std::vector<std::array<V3, 3>> load_ply(const std::string& path) {
+  PlyIn in(path);
+  if (trimmed(in.line()) != "ply") throw std::runtime_error("ply magic number not found");
+  int fmt = 0;
+  struct Prop {
+    bool list;
+    std::string name, t, ct;
+  };
+  struct El {
+    std::string name;
+    size_t n;
+    std::vector<Prop> props;
+  };
+  std::vector<El> els;
+  for (;;) {
+    std::string l = in.line();
+    if (l.empty()) throw std::runtime_error("ply header eof");
+    auto sp = split1(trimmed(l));
+    if (sp[0] == "end_header") break;
+    if (sp[0] == "format") {
+      if (sp.size() > 2 && sp[1] == "ascii" && sp[2] == "1.0")
+        fmt = 0;
+      else if (sp.size() > 2 && sp[1] == "binary_little_endian" && sp[2] == "1.0")
+        fmt = 1;
+      else if (sp.size() > 2 && sp[1] == "binary_big_endian" && sp[2] == "1.0")
+        fmt = 2;
+      else
+        throw std::runtime_error("ply unsupported format");
+    } else if (sp[0] == "element") {
+      els.push_back(El{sp.at(1), (size_t)std::stoull(sp.at(2)), {}});
+    } else if (sp[0] == "property" && !els.empty()) {
+      if (sp.at(1) == "list")
+        els.back().props.push_back(Prop{true, sp.at(4), sp.at(3), sp.at(2)});
+      else
+        els.back().props.push_back(Prop{false, sp.at(2), sp.at(1), ""});
+    }
+  }
+  std::vector<V3> verts;
+  std::vector<std::array<V3, 3>> faces;
+  auto rd_f = [&](const std::string& t) -> float {
+    if (fmt == 0) return strtof(in.word().c_str(), nullptr);
+    return (float)ply_bin(in, t, fmt == 2);
+  };
+  auto rd_u = [&](const std::string& t) -> uint64_t {
+    if (fmt == 0) return (uint64_t)strtoull(in.word().c_str(), nullptr, 10);
+    double d = ply_bin(in, t, fmt == 2);
+    return d > 0 ? (uint64_t)d : 0;
+  };
+  for (const El& e : els) {
+    for (size_t i = 0; i < e.n; ++i) {
+      float xyz[3] = {0, 0, 0};
+      int have = 0;
+      for (const Prop& p : e.props) {
+        if (!p.list) {
+          int k = e.name == "vertex" ? (p.name == "x" ? 0 : p.name == "y" ? 1 : p.name == "z" ? 2 : -1) : -1;
+          if (k >= 0) {
+            xyz[k] = rd_f(p.t);
+            have |= 1 << k;
+          } else if (fmt == 0) {
+            in.word();
+          } else {
+            ply_bin(in, p.t, fmt == 2);
+          }
+        } else {
+          uint64_t cnt = rd_u(p.ct);
+          if (e.name == "face" && cnt == 3) {
+            uint64_t a = rd_u(p.t), b = rd_u(p.t), c = rd_u(p.t);
+            faces.push_back({verts.at(a), verts.at(b), verts.at(c)});
+          } else {
+            for (uint64_t k = 0; k < cnt; ++k) fmt == 0 ? (void)in.word() : (void)ply_bin(in, p.t, fmt == 2);
+          }
+        }
+      }
+      if (e.name == "vertex" && have == 7) verts.push_back(V3{xyz[0], xyz[1], xyz[2]});
+    }
+  }
+  return faces;
+}
+
+// obj_loader.rs:332-452 with obj_fns (identity)
+struct ObjTri {
+  V3 v[3], n[3];
+  V2 uv[3];
+};
+std::vector<ObjTri> load_obj(const std::string& path) {
+  std::ifstream in(path);
+  if (!in) throw std::runtime_error("cannot open " + path);
+  std::vector<V3> vs, ns;
+  std::vector<V2> uvs;
+  std::vector<ObjTri> out;
+  std::string line;
+  auto num = [](const std::string& s, uint64_t& v) {
+    size_t i = (!s.empty() && s[0] == '+') ? 1 : 0;
+    if (i >= s.size()) return false;
+    v = 0;
+    for (; i < s.size(); ++i) {
+      if (!isdigit((unsigned char)s[i])) return false;
+      v = v * 10 + (s[i] - '0');
+    }
+    return true;
+  };
+  while (std::getline(in, line)) {
+    std::vector<std::string> p;
+    {
+      std::string cur;
+      for (char ch : line) {
+        if (isspace((unsigned char)ch)) {
+          if (!cur.empty()) p.push_back(cur), cur.clear();
+        } else {
+          cur.push_back(ch);
+        }
+      }
+      if (!cur.empty()) p.push_back(cur);
+    }
+    if (p.empty()) continue;
+    if (p[0] == "v" || p[0] == "vn") {
+      if (p.size() < 4) throw std::runtime_error("unable to parse vertex");
+      V3 v{strtof(p[1].c_str(), nullptr), strtof(p[2].c_str(), nullptr), strtof(p[3].c_str(), nullptr)};
+      (p[0] == "v" ? vs : ns).push_back(v);
+    } else if (p[0] == "vt") {
+      if (p.size() < 3) throw std::runtime_error("unable to parse texture coord");
+      uvs.push_back(V2{strtof(p[1].c_str(), nullptr), strtof(p[2].c_str(), nullptr)});
+    } else if (p[0] == "f") {
+      if (p.size() < 4) throw std::runtime_error("unable to parse face");
+      ObjTri t;
+      for (int k = 0; k < 3; ++k) {
+        const std::string& s = p[k + 1];
+        std::vector<uint64_t> idx;
+        size_t st = 0;
+        for (;;) {
+          size_t q = s.find('/', st);
+          uint64_t v;
+          if (num(s.substr(st, q == std::string::npos ? std::string::npos : q - st), v)) idx.push_back(v);
+          if (q == std::string::npos) break;
+          st = q + 1;
+        }
+        if (s.find("//") != std::string::npos) {
+          if (idx.size() < 2 || uvs.empty()) throw std::runtime_error("unable to parse face");
+          t.v[k] = vs.at(idx[0] - 1), t.n[k] = ns.at(idx[1] - 1), t.uv[k] = uvs[0];
+        } else {
+          if (idx.size() < 3) throw std::runtime_error("unable to parse face");
+          t.v[k] = vs.at(idx[0] - 1), t.uv[k] = uvs.at(idx[1] - 1), t.n[k] = ns.at(idx[2] - 1);
+        }
+      }
+      out.push_back(t);
+    }
+  }
+  return out;
+}
+
+bool png_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_t& w, uint32_t& h) {
+  std::ifstream in(path, std::ios::binary);
+  std::vector<uint8_t> d((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+  if (d.size() < 8) return false;
+  auto be = [](const uint8_t* p) { return (uint32_t)p[0] << 24 | p[1] << 16 | p[2] << 8 | p[3]; };
+  std::vector<uint8_t> z;
+  int ct = -1;
+  for (size_t p = 8; p + 8 <= d.size();) {
+    uint32_t n = be(&d[p]);
+    std::string t((char*)&d[p + 4], 4);
+    if (t == "IHDR") {
+      w = be(&d[p + 8]), h = be(&d[p + 12]), ct = d[p + 17];
+      if (d[p + 16] != 8 || d[p + 20] != 0) return false;
+    } else if (t == "IDAT") {
+      z.insert(z.end(), &d[p + 8], &d[p + 8] + n);
+    }
+    p += 12 + n;
+  }
+  int ch = ct == 6 ? 4 : ct == 2 ? 3 : ct == 0 ? 1 : ct == 4 ? 2 : 0;
+  if (!ch) return false;
+  size_t stride = (size_t)w * ch;
+  std::vector<uint8_t> raw((stride + 1) * h);
+  uLongf len = raw.size();
+  if (uncompress(raw.data(), &len, z.data(), z.size()) != Z_OK) return false;
+  std::vector<uint8_t> img(stride * h);
+  for (uint32_t y = 0; y < h; ++y) {
+    uint8_t f = raw[y * (stride + 1)];
+    for (size_t x = 0; x < stride; ++x) {
+      int a = x >= (size_t)ch ? img[y * stride + x - ch] : 0;
+      int b = y ? img[(y - 1) * stride + x] : 0;
+      int c = (x >= (size_t)ch && y) ? img[(y - 1) * stride + x - ch] : 0;
+      int pr = 0;
+      if (f == 1) pr = a;
+      if (f == 2) pr = b;
+      if (f == 3) pr = (a + b) >> 1;
+      if (f == 4) {
+        int pp = a + b - c, pa = abs(pp - a), pb = abs(pp - b), pc = abs(pp - c);
+        pr = (pa <= pb && pa <= pc) ? a : pb <= pc ? b : c;
+      }
+      img[y * stride + x] = (uint8_t)(raw[y * (stride + 1) + 1 + x] + pr);
+    }
+  }
+  rgba.resize((size_t)w * h * 4);
+  for (size_t i = 0; i < (size_t)w * h; ++i) {
+    const uint8_t* s = &img[i * ch];
+    uint8_t* o = &rgba[4 * i];
+    if (ch == 4) memcpy(o, s, 4);
+    if (ch == 3) o[0] = s[0], o[1] = s[1], o[2] = s[2], o[3] = 255;
+    if (ch == 1) o[0] = o[1] = o[2] = s[0], o[3] = 255;
+    if (ch == 2) o[0] = o[1] = o[2] = s[0], o[3] = s[1];
+  }
+  return true;
+}
+}  // namespace
+
+// --------------------------------------------------------------- builder
+static std::shared_ptr<Material> mat(orc_scene* s, uint32_t i) {
+  if (i >= s->materials.size()) throw std::runtime_error("material index out of range");
+  return s->materials[i];
+}
+
+static void add_sphere(orc_scene* s, std::shared_ptr<Material> m, V3 c, float r) {
+  auto* sp = new Sphere();
+  sp->center = c, sp->radius = r, sp->material = std::move(m), sp->id = s->n_spheres++;
+  s->world.objects.push_back(Obj(sp));
+}
+
+static Triangle* new_tri(orc_scene* s, std::shared_ptr<Material> m, V3 a, V3 b, V3 c) {  // Triangle::new
+  auto* t = new Triangle();
+  t->a = a, t->b = b, t->c = c, t->material = std::move(m);
+  V3 n = unit(cross(b - a, c - a));
+  t->na = t->nb = t->nc = n;
+  t->id = s->n_tris++;
+  return t;
+}
+
+static Triangle* new_tri_uv(orc_scene* s, std::shared_ptr<Material> m, const float* f) {  // with_norms_and_uvs
+  auto* t = new Triangle();
+  t->a = v3p(f), t->na = v3p(f + 3), t->uva = V2{f[6], f[7]};
+  t->b = v3p(f + 8), t->nb = v3p(f + 11), t->uvb = V2{f[14], f[15]};
+  t->c = v3p(f + 16), t->nc = v3p(f + 19), t->uvc = V2{f[22], f[23]};
+  V3 ab = t->b - t->a, ac = t->c - t->a;
+  V2 uab = t->uvb - t->uva, uac = t->uvc - t->uva;
+  float r = fmaxf(fminf(1.0f / (uab.x * uac.y - uab.y * uac.x), 1.0f), -1.0f);
+  t->tangent = (ab * uac.y - ac * uab.y) * r;
+  t->bitangent = (ac * uab.x - ab * uac.x) * r;
+  t->has_uv = true;
+  t->material = std::move(m);
+  t->id = s->n_tris++;
+  return t;
+}
+
+static int make_model(orc_scene* s, std::vector<Obj> tris, std::shared_ptr<Material> override_m, bool add) {
+  if (tris.empty()) throw std::runtime_error("empty model");
+  auto node = std::make_shared<BvhNode>(std::move(tris), s->rng);
+  s->blas.push_back(node);
+  s->model_override.push_back(override_m);
+  if (add) {
+    auto* m = new Model();
+    m->tris = node, m->material = override_m, m->id = s->n_models++;
+    s->world.objects.push_back(Obj(m));
+  }
+  return (int)s->blas.size() - 1;
+}
+
+static void add_instance(orc_scene* s, int model, V3 t, V3 r, V3 sc, std::shared_ptr<Material> m) {
+  auto* in = new Instance(s->blas.at(model), t, r, sc);
+  in->material = std::move(m);
+  in->id = s->n_inst++;
+  s->world.objects.push_back(Obj(in));
+}
+
+static std::vector<Obj> ply_tris(orc_scene* s, const std::string& path, std::shared_ptr<Material> m) {
+  std::vector<Obj> v;
+  for (auto& f : load_ply(path)) v.push_back(Obj(new_tri(s, m, f[0], f[1], f[2])));
+  return v;
+}
+
+static std::string jp(const std::string& d, const std::string& n) { return d.empty() ? n : d + "/" + n; }
+
+static std::shared_ptr<Surface> solid(V4 c) { return std::make_shared<SolidColor>(c); }
+static std::shared_ptr<Material> lamb(V4 c) { return std::make_shared<Lambertian>(solid(c)); }
+
+// scenes/*.rs restated (see mass-raytrace_amd/csrc/host/scenes.cpp for the
+// configuration notes of the scenes that are not in the reference)
+static void builtin(orc_scene* s, const std::string& name, float aspect, const std::string& dir) {
+  auto none = std::make_shared<NoMaterial>();
+  auto white = lamb(V4{1, 1, 1, 1});
+  auto cam_at = [&](float fov, V3 from, V3 at) {
+    s->camera = Camera::make(fov, from, at, V3{0, 1, 0}, aspect, 0.0f, length(from - at));
+  };
+  if (name == "sphere_grid") {  // sphere_grid.rs:23-94
+    int cube = make_model(s, ply_tris(s, jp(dir, "cube.ply"), none), nullptr, false);
+    add_instance(s, cube, V3{0, -1000, 0}, V3{0, 0, 0}, fill(1000), white);
+    float r = 1.0f, d = r * 2.0f, a = sqrtf(d * d - r * r);
+    for (int i = -50; i < 50; ++i)
+      for (int j = -50; j < 50; ++j) {
+        float off = j % 2 == 0 ? r : 0.0f;
+        V3 c{((float)i * d) + off, r, (float)j * a};
+        float rr = r - 0.05f;
+        if (i == 0 && j == 0)
+          add_sphere(s, std::make_shared<DiffuseLight>(fill(3.0f)), c, rr);
+        else if ((i == -1 && j == 0) || (i == 1 && j == 0) || (i == 1 && j == -1) || (i == 0 && j == -1) ||
+                 (i == 1 && j == 1) || (i == 0 && j == 1))
+          add_sphere(s, std::make_shared<Dielectric>(1.8f), c, rr);
+        else {
+          float x = s->rng.f32(), y = s->rng.f32(), z = s->rng.f32();
+          add_sphere(s, std::make_shared<Metal>(0.0f, solid(V4{x, y, z, 1.0f})), c, rr);
+        }
+      }
+    cam_at(40.0f, V3{6, 8, 5}, V3{0, 0, 0});
+  } else if (name == "cornell") {  // cornell.rs:20-99
+    int cube = make_model(s, ply_tris(s, jp(dir, "cube.ply"), none), nullptr, false);
+    add_instance(s, cube, V3{-10, 5, 0}, V3{0, 0, 0}, fill(5), lamb(V4{1, 0, 0, 1}));
+    add_instance(s, cube, V3{10, 5, 0}, V3{0, 0, 0}, fill(5), lamb(V4{0, 1, 0, 1}));
+    add_instance(s, cube, V3{0, 15, 0}, V3{0, 0, 0}, fill(5), white);
+    add_instance(s, cube, V3{0, 5, -10}, V3{0, 0, 0}, fill(5), white);
+    add_instance(s, cube, V3{0, -5, -0.0f}, V3{0, 0, 0}, fill(5), white);
+    add_sphere(s, std::make_shared<Dielectric>(1.3f), V3{1.75f, 2.0f, 2.25f}, 2.0f);
+    add_instance(s, cube, V3{0, 10.0f - 0.00011f, 0}, V3{0, 0, 0}, V3{1, 0.0001f, 1},
+                 std::make_shared<DiffuseLight>(fill(8.0f)));
+    add_instance(s, cube, V3{-2, 3, -1}, V3{0, -0.05f, 0}, V3{1.75f, 3.1f, 1.75f}, white);
+    cam_at(37.0f, V3{0, 5, 20}, V3{0, 5, 0});
+  } else if (name == "cube_field") {
+    int cube = make_model(s, ply_tris(s, jp(dir, "cube.ply"), none), nullptr, false);
+    add_instance(s, cube, V3{0, -1000, 0}, V3{0, 0, 0}, fill(1000), white);
+    int k = 0;
+    for (int x = -50; x < 50; ++x)
+      for (int z = -50; z < 50; ++z, ++k) {
+        std::shared_ptr<Material> m;
+        if (k % 3 == 0) {
+          float r = 1.0f - (s->rng.f32() * 0.5f);
+          float g = 1.0f - (s->rng.f32() * 0.5f);
+          float b = 1.0f - (s->rng.f32() * 0.5f);
+          m = lamb(V4{r, g, b, 1.0f});
+        } else if (k % 3 == 1) {
+          float r = s->rng.f32(), g = s->rng.f32(), b = s->rng.f32();
+          m = std::make_shared<Metal>(0.3f, solid(V4{r, g, b, 1.0f}));
+        } else {
+          m = std::make_shared<Dielectric>(1.5f);
+        }
+        float yaw = s->rng.f32();
+        add_instance(s, cube, V3{(float)x * 3.0f, 1.0f, (float)z * 3.0f}, V3{0, yaw, 0}, fill(1.0f), m);
+      }
+    add_sphere(s, std::make_shared<DiffuseLight>(V3{4, 4, 5} * 10.0f), V3{10000, 4000, 4800}, 1500);
+    cam_at(40.0f, V3{6, 8, 5}, V3{0, 0, 0});
+  } else if (name == "mesh_ply" || name == "mesh_obj" || name == "mesh_obj_textured") {
+    bool textured = name == "mesh_obj_textured";
+    std::shared_ptr<Surface> albedo;
+    if (textured) {
+      std::vector<uint8_t> px;
+      uint32_t w, h;
+      if (!png_rgba(jp(dir, "env_4096x2048.png"), px, w, h)) throw std::runtime_error("env png");
+      s->world.background.reset(new SkySphere(std::make_shared<Texture>(px.data(), w, h, WRAP_REPEAT)));
+      if (!png_rgba(jp(dir, "albedo_2048.png"), px, w, h)) throw std::runtime_error("albedo png");
+      albedo = std::make_shared<Texture>(px.data(), w, h, WRAP_REPEAT);
+    }
+    int cube = make_model(s, ply_tris(s, jp(dir, "cube.ply"), none), nullptr, false);
+    if (name == "mesh_ply") {
+      make_model(s, ply_tris(s, jp(dir, "mesh_1m.ply"), none), lamb(V4{0.8f, 0.6f, 0.4f, 1.0f}), true);
+    } else {
+      std::shared_ptr<Material> m =
+          textured ? std::shared_ptr<Material>(std::make_shared<Lambertian>(albedo)) : lamb(V4{0.8f, 0.6f, 0.4f, 1.0f});
+      std::vector<Obj> tris;
+      for (const ObjTri& t : load_obj(jp(dir, "mesh_1m.obj"))) {
+        float f[24];
+        for (int k = 0; k < 3; ++k) {
+          f[8 * k] = t.v[k].x, f[8 * k + 1] = t.v[k].y, f[8 * k + 2] = t.v[k].z;
+          f[8 * k + 3] = t.n[k].x, f[8 * k + 4] = t.n[k].y, f[8 * k + 5] = t.n[k].z;
+          f[8 * k + 6] = t.uv[k].x, f[8 * k + 7] = t.uv[k].y;
+        }
+        tris.push_back(Obj(new_tri_uv(s, m, f)));
+      }
+      make_model(s, std::move(tris), nullptr, true);
+    }
+    add_instance(s, cube, V3{0, -1001, 0}, V3{0, 0, 0}, fill(1000), white);
+    if (!textured) {
+      auto light = std::make_shared<DiffuseLight>(fill(8.0f));
+      add_instance(s, cube, V3{-2.5f, 4.0f, 0.0f}, V3{0, 0, 0}, V3{1.0f, 0.0001f, 1.0f}, light);
+      add_instance(s, cube, V3{2.5f, 4.0f, 1.0f}, V3{0, 0, 0}, V3{1.0f, 0.0001f, 1.0f}, light);
+    }
+    cam_at(40.0f, V3{0.0f, 3.2f, 6.5f}, V3{0.0f, -0.2f, 0.0f});
+  } else {
+    throw std::runtime_error("unknown scene " + name);
+  }
+  std::vector<Obj> objs = std::move(s->world.objects);  // World::build_bvh
+  s->world.objects.clear();
+  s->world.objects.push_back(Obj(new BvhNode(std::move(objs), s->rng)));
+}
+
+extern "C" {
+
+orc_scene* orc_new(uint64_t seed) {
+  auto* s = new orc_scene();
+  s->rng.s = seed;
+  return s;
+}
+void orc_free(orc_scene* s) { delete s; }
+float orc_rand_f32(orc_scene* s) { return s->rng.f32(); }
+
+int orc_builtin(orc_scene* s, const char* name, float aspect, const char* dir) {
+  return guard([&] {
+    builtin(s, name, aspect, dir ? dir : "");
+    return 0;
+  });
+}
+
+int orc_solid(orc_scene* s, float r, float g, float b, float a) {
+  s->surfaces.push_back(solid(V4{r, g, b, a}));
+  return (int)s->surfaces.size() - 1;
+}
+int orc_texture_rgba(orc_scene* s, const uint8_t* rgba, uint32_t w, uint32_t h, uint32_t wrap) {
+  s->surfaces.push_back(std::make_shared<Texture>(rgba, w, h, wrap));
+  return (int)s->surfaces.size() - 1;
+}
+int orc_texture_png(orc_scene* s, const char* path, uint32_t wrap) {
+  std::vector<uint8_t> px;
+  uint32_t w, h;
+  if (!png_rgba(path, px, w, h)) return -1;
+  return orc_texture_rgba(s, px.data(), w, h, wrap);
+}
+int orc_material(orc_scene* s, uint32_t kind, uint32_t surface, float param, float er, float eg, float eb) {
+  return guard([&] {
+    std::shared_ptr<Material> m;
+    auto surf = [&]() {
+      if (surface >= s->surfaces.size()) throw std::runtime_error("surface out of range");
+      return s->surfaces[surface];
+    };
+    switch (kind) {
+      case 0:
+        m = std::make_shared<NoMaterial>();
+        break;
+      case 1:
+        m = std::make_shared<Lambertian>(surf());
+        break;
+      case 2:
+        m = std::make_shared<Metal>(param, surf());
+        break;
+      case 3:
+        m = std::make_shared<Dielectric>(param);
+        break;
+      case 4:
+        m = std::make_shared<DiffuseLight>(V3{er, eg, eb});
+        break;
+      default:
+        throw std::runtime_error("bad material kind");
+    }
+    s->materials.push_back(m);
+    return (int)s->materials.size() - 1;
+  });
+}
+int orc_background(orc_scene* s, uint32_t kind, uint32_t surface, float r, float g, float b) {
+  return guard([&] {
+    if (kind == 0)
+      s->world.background.reset(new SolidBackground(V3{r, g, b}));
+    else if (kind == 1)
+      s->world.background.reset(new SkyBackground());
+    else
+      s->world.background.reset(new SkySphere(s->surfaces.at(surface)));
+    return 0;
+  });
+}
+int orc_add_sphere(orc_scene* s, uint32_t m, float cx, float cy, float cz, float r) {
+  return guard([&] {
+    add_sphere(s, mat(s, m), V3{cx, cy, cz}, r);
+    return 0;
+  });
+}
+int orc_add_triangle(orc_scene* s, uint32_t m, const float* abc) {
+  return guard([&] {
+    s->world.objects.push_back(Obj(new_tri(s, mat(s, m), v3p(abc), v3p(abc + 3), v3p(abc + 6))));
+    return 0;
+  });
+}
+int orc_model(orc_scene* s, uint32_t tri_m, uint32_t over, const float* tris, uint32_t n, int shading, int add) {
+  return guard([&] {
+    std::vector<Obj> v;
+    auto m = mat(s, tri_m);
+    for (uint32_t i = 0; i < n; ++i) {
+      if (shading)
+        v.push_back(Obj(new_tri_uv(s, m, tris + 24 * (size_t)i)));
+      else {
+        const float* t = tris + 9 * (size_t)i;
+        v.push_back(Obj(new_tri(s, m, v3p(t), v3p(t + 3), v3p(t + 6))));
+      }
+    }
+    return make_model(s, std::move(v), over == 0xFFFFFFFFu ? nullptr : mat(s, over), add != 0);
+  });
+}
+int orc_model_from_ply(orc_scene* s, const char* path, uint32_t tri_m, uint32_t over, int add) {
+  return guard([&] {
+    return make_model(s, ply_tris(s, path, mat(s, tri_m)), over == 0xFFFFFFFFu ? nullptr : mat(s, over), add != 0);
+  });
+}
+int orc_add_instance(orc_scene* s, int model, const float* t, const float* r, const float* sc, uint32_t m) {
+  return guard([&] {
+    add_instance(s, model, v3p(t), v3p(r), v3p(sc), m == 0xFFFFFFFFu ? nullptr : mat(s, m));
+    return 0;
+  });
+}
+int orc_camera(orc_scene* s, float vfov, const float* from, const float* at, const float* up, float aspect,
+               float aperture, float focus) {
+  s->camera = Camera::make(vfov, v3p(from), v3p(at), v3p(up), aspect, aperture, focus);
+  return 0;
+}
+int orc_build_bvh(orc_scene* s) {
+  return guard([&] {
+    std::vector<Obj> objs = std::move(s->world.objects);
+    s->world.objects.clear();
+    s->world.objects.push_back(Obj(new BvhNode(std::move(objs), s->rng)));
+    return 0;
+  });
+}
+int orc_camera_fields(orc_scene* s, float* o) {
+  const Camera& c = s->camera;
+  V3 f[6] = {c.origin, c.llc, c.horizontal, c.vertical, c.u, c.v};
+  for (int i = 0; i < 6; ++i) o[3 * i] = f[i].x, o[3 * i + 1] = f[i].y, o[3 * i + 2] = f[i].z;
+  o[18] = c.lens_radius;
+  return 0;
+}
+
+static int64_t copy_sink(const PreorderSink& k, uint32_t* kinds, float* boxes, uint64_t cap) {
+  uint64_t n = k.kinds.size() / 2;
+  if (kinds && boxes) {
+    uint64_t m = std::min(n, cap);
+    memcpy(kinds, k.kinds.data(), m * 8);
+    memcpy(boxes, k.boxes.data(), m * 24);
+  }
+  return (int64_t)n;
+}
+int64_t orc_export_preorder(orc_scene* s, uint32_t* kinds, float* boxes, uint64_t cap) {
+  PreorderSink k;
+  for (const Obj& o : s->world.objects) o->preorder(k);
+  return copy_sink(k, kinds, boxes, cap);
+}
+int64_t orc_blas_count(orc_scene* s) { return (int64_t)s->blas.size(); }
+int64_t orc_export_blas(orc_scene* s, int64_t b, uint32_t* kinds, float* boxes, uint64_t cap) {
+  if (b < 0 || (size_t)b >= s->blas.size()) return -1;
+  PreorderSink k;
+  s->blas[b]->preorder(k);
+  return copy_sink(k, kinds, boxes, cap);
+}
+
+int orc_trace_rays(orc_scene* s, const float* rays, uint32_t n, float tmin, float tmax, orc_hit* out) {
+  return guard([&] {
+    Ctx c;
+    for (uint32_t i = 0; i < n; ++i) {
+      Ray r{v3p(rays + 6 * (size_t)i), v3p(rays + 6 * (size_t)i + 3)};
+      Hit h;
+      if (s->world.intersect(r, tmin, tmax, h, c)) {
+        out[i] = orc_hit{h.prim, h.container, h.t, h.front_face ? 1u : 0u};
+      } else {
+        out[i] = orc_hit{0, 0, 0.0f, 0};
+      }
+    }
+    std::lock_guard<std::mutex> g(s->mu);
+    s->counters.add(c.cnt);
+    return 0;
+  });
+}
+
+// main.rs:257-263 for pixel p, sample `sample`
+static void sample_pixel(const orc_scene* s, uint32_t W, uint32_t H, uint32_t p, uint32_t sample, uint64_t seed,
+                         uint32_t max_depth, Ctx& c, V3& color, uint32_t& bounces) {
+  uint32_t x = p % W, y = p / W;
+  PathRng rng(seed, p, sample);
+  c.rng = &rng;
+  float u = ((float)x + c.rand()) / (float)(W - 1);
+  float v = ((float)y + c.rand()) / (float)(H - 1);
+  Ray ray = s->camera.ray(u, v, c);
+  auto r = trace(s->world, ray, max_depth, c);
+  color = r.first;
+  bounces = max_depth - r.second;
+  c.cnt.samples++;
+}
+
+static void run_threads(int threads, uint32_t n, const std::function<void(uint32_t, uint32_t)>& body) {
+  if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  std::atomic<uint32_t> next{0};
+  std::vector<std::thread> ts;
+  const uint32_t chunk = 64;
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&] {
+      for (;;) {
+        uint32_t b = next.fetch_add(chunk);
+        if (b >= n) return;
+        body(b, std::min(n, b + chunk));
+      }
+    });
+  for (auto& t : ts) t.join();
+}
+
+int orc_render_pixels(orc_scene* s, uint32_t W, uint32_t H, const uint32_t* pixels, uint32_t n, uint32_t spp_begin,
+                      uint32_t spp_count, uint64_t seed, uint32_t max_depth, int threads, float* out_rgb,
+                      uint32_t* out_b) {
+  return guard([&] {
+    std::exception_ptr err;
+    run_threads(threads, n, [&](uint32_t b, uint32_t e) {
+      Ctx c;
+      try {
+        for (uint32_t i = b; i < e; ++i) {
+          float r = out_rgb[3 * (size_t)i], g = out_rgb[3 * (size_t)i + 1], bl = out_rgb[3 * (size_t)i + 2];
+          uint32_t k = out_b[i];
+          for (uint32_t sm = 0; sm < spp_count; ++sm) {
+            V3 col;
+            uint32_t bo;
+            sample_pixel(s, W, H, pixels[i], spp_begin + sm, seed, max_depth, c, col, bo);
+            r = r + col.x, g = g + col.y, bl = bl + col.z;  // Image::merge (main.rs:629-638)
+            k += bo;
+          }
+          out_rgb[3 * (size_t)i] = r, out_rgb[3 * (size_t)i + 1] = g, out_rgb[3 * (size_t)i + 2] = bl;
+          out_b[i] = k;
+        }
+      } catch (...) {
+        std::lock_guard<std::mutex> gl(s->mu);
+        err = std::current_exception();
+      }
+      std::lock_guard<std::mutex> gl(s->mu);
+      if (s->counting) s->counters.add(c.cnt);
+    });
+    if (err) std::rethrow_exception(err);
+    return 0;
+  });
+}
+
+int orc_render(orc_scene* s, uint32_t W, uint32_t H, uint32_t spp_begin, uint32_t spp_count, uint64_t seed,
+               uint32_t max_depth, uint32_t si, uint32_t sc, int threads, float* rgb, uint32_t* b) {
+  return guard([&] {
+    if (sc == 0) sc = 1;
+    uint32_t tx = (W + 7) / 8;
+    std::vector<uint32_t> px;
+    for (uint32_t y = 0; y < H; ++y)
+      for (uint32_t x = 0; x < W; ++x)
+        if (((y / 8) * tx + (x / 8)) % sc == si) px.push_back(y * W + x);
+    std::vector<float> o(px.size() * 3);
+    std::vector<uint32_t> ob(px.size());
+    for (size_t i = 0; i < px.size(); ++i) {
+      for (int k = 0; k < 3; ++k) o[3 * i + k] = rgb[3 * (size_t)px[i] + k];
+      ob[i] = b[px[i]];
+    }
+    int rc = orc_render_pixels(s, W, H, px.data(), (uint32_t)px.size(), spp_begin, spp_count, seed, max_depth,
+                               threads, o.data(), ob.data());
+    if (rc) return rc;
+    for (size_t i = 0; i < px.size(); ++i) {
+      for (int k = 0; k < 3; ++k) rgb[3 * (size_t)px[i] + k] = o[3 * i + k];
+      b[px[i]] = ob[i];
+    }
+    return 0;
+  });
+}
+
+// main.rs:150-290 threading: every worker renders whole 1-spp passes of the
+// (row-restricted) frame into its own ImageBuffer, then merges under a Mutex.
+double orc_bench_reference_mode(orc_scene* s, uint32_t W, uint32_t H, uint32_t passes, uint64_t seed,
+                                uint32_t max_depth, int threads, float* rgb, uint32_t* bo, uint32_t row_begin,
+                                uint32_t row_end) {
+  if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  if (row_end > H || row_end == 0) row_end = H;
+  std::mutex image_mu;
+  std::atomic<uint32_t> pass_counter{0};
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> ts;
+  std::atomic<bool> failed{false};
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&] {
+      std::vector<std::pair<V3, uint32_t>> buffer((size_t)W * H);
+      Ctx c;
+      try {
+        for (uint32_t k = 0; k < passes; ++k) {
+          uint32_t sample = pass_counter.fetch_add(1);
+          for (uint32_t y = row_begin; y < row_end; ++y)
+            for (uint32_t x = 0; x < W; ++x) {
+              uint32_t p = y * W + x;
+              sample_pixel(s, W, H, p, sample, seed, max_depth, c, buffer[p].first, buffer[p].second);
+            }
+          std::lock_guard<std::mutex> g(image_mu);
+          for (uint32_t y = row_begin; y < row_end; ++y)
+            for (uint32_t x = 0; x < W; ++x) {
+              size_t p = (size_t)y * W + x;
+              rgb[3 * p] += buffer[p].first.x, rgb[3 * p + 1] += buffer[p].first.y, rgb[3 * p + 2] += buffer[p].first.z;
+              bo[p] += buffer[p].second;
+            }
+        }
+      } catch (...) {
+        failed = true;
+      }
+      std::lock_guard<std::mutex> g(s->mu);
+      s->counters.add(c.cnt);
+    });
+  for (auto& t : ts) t.join();
+  double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return failed ? -1.0 : secs;
+}
+
+void orc_get_counters(orc_scene* s, orc_counters* o) {
+  const Counters& c = s->counters;
+  *o = orc_counters{c.samples,        c.segments,      c.node_visits,  c.sphere_tests, c.triangle_tests, c.instance_entries,
+                    c.model_entries, c.closest_hits, c.texel_taps, c.bounces,      c.alpha_taps};
+}
+void orc_reset_counters(orc_scene* s) { s->counters = Counters{}; }
+void orc_set_counting(orc_scene* s, int on) { s->counting = on != 0; }
+
+}  // extern "C"

@@ -1,0 +1,93 @@
+// oracle.h — TEST INFRASTRUCTURE ONLY. CPU restatement of the reference's
+// path-tracing hot path (nickmass/mass-raytrace, Rust) used as the parity
+// checker and the CPU baseline. Only tests/, __graft_entry__.smoke() and
+// bench.py's cpu_baseline leg may load it; the product (libmassrt.so) never
+// links or calls it.
+//
+// Parity status: the reference has no tests, golden vectors or fixtures other
+// than cube.ply, and it cannot be built here (Rust toolchain
+// and 215 crates absent). This restatement is therefore pinned only by
+// cube.ply, hand-derived known answers (analytic sphere/triangle hits, BVH
+// node counts, furnace scenes) and the fastrand algorithm as published:
+// PARITY UNPINNED against the reference binary itself.
+//
+// Structure follows the reference on purpose (and unlike the product):
+// heap-allocated objects behind virtual `intersect`, recursive left-first
+// BvhNode traversal, recursive Camera::trace with post-order radiance fold.
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_scene orc_scene;
+
+typedef struct {
+  uint64_t samples, segments, node_visits, sphere_tests, triangle_tests, instance_entries, model_entries,
+      closest_hits, texel_taps, bounces, alpha_taps;
+} orc_counters;
+
+typedef struct {
+  uint32_t prim, container;
+  float t;
+  uint32_t front_face;
+} orc_hit;
+
+const char* orc_last_error(void);
+
+// scene construction ---------------------------------------------------------
+orc_scene* orc_new(uint64_t rng_seed);
+void orc_free(orc_scene* s);
+int orc_builtin(orc_scene* s, const char* name, float aspect, const char* asset_dir);
+float orc_rand_f32(orc_scene* s);
+int orc_solid(orc_scene* s, float r, float g, float b, float a);
+int orc_texture_rgba(orc_scene* s, const uint8_t* rgba, uint32_t w, uint32_t h, uint32_t wrap);
+int orc_texture_png(orc_scene* s, const char* path, uint32_t wrap);
+int orc_material(orc_scene* s, uint32_t kind, uint32_t surface, float param, float er, float eg, float eb);
+int orc_background(orc_scene* s, uint32_t kind, uint32_t surface, float r, float g, float b);
+int orc_add_sphere(orc_scene* s, uint32_t material, float cx, float cy, float cz, float radius);
+int orc_add_triangle(orc_scene* s, uint32_t material, const float* abc);
+int orc_model(orc_scene* s, uint32_t tri_material, uint32_t override_material, const float* tris, uint32_t n,
+              int with_shading, int add_to_world);
+int orc_model_from_ply(orc_scene* s, const char* path, uint32_t tri_material, uint32_t override_material,
+                       int add_to_world);
+int orc_add_instance(orc_scene* s, int model, const float* t, const float* r, const float* sc, uint32_t material);
+int orc_camera(orc_scene* s, float vfov, const float* from, const float* at, const float* up, float aspect,
+               float aperture, float focus);
+int orc_build_bvh(orc_scene* s);
+// camera fields: origin, llc, horizontal, vertical, u, v (18 floats) + lens radius
+int orc_camera_fields(orc_scene* s, float* out19);
+
+// preorder listing of the world tree: per element {kind, index} (kind: 1 node,
+// 2 sphere, 3 triangle, 4 instance, 5 model, 6 end-of-node) and for nodes the
+// 6 box floats. Returns element count (call with NULL to size).
+int64_t orc_export_preorder(orc_scene* s, uint32_t* kinds_ids, float* boxes, uint64_t cap);
+// same for the BLAS of model `m` (index in creation order of models/instances' BLAS)
+int64_t orc_blas_count(orc_scene* s);
+int64_t orc_export_blas(orc_scene* s, int64_t blas, uint32_t* kinds_ids, float* boxes, uint64_t cap);
+
+// hot path ---------------------------------------------------------------------
+int orc_trace_rays(orc_scene* s, const float* rays, uint32_t n, float tmin, float tmax, orc_hit* out);
+// Deterministic render: samples [spp_begin, spp_begin+spp_count) of every pixel
+// of the shard added in sample order (same contract as mrt_render).
+int orc_render(orc_scene* s, uint32_t W, uint32_t H, uint32_t spp_begin, uint32_t spp_count, uint64_t seed,
+               uint32_t max_depth, uint32_t shard_index, uint32_t shard_count, int threads, float* accum_rgb,
+               uint32_t* accum_bounces);
+// Same, for an explicit list of pixel indices (p = y*W + x); out_rgb n*3, out_b n (added to).
+int orc_render_pixels(orc_scene* s, uint32_t W, uint32_t H, const uint32_t* pixels, uint32_t n, uint32_t spp_begin,
+                      uint32_t spp_count, uint64_t seed, uint32_t max_depth, int threads, float* out_rgb,
+                      uint32_t* out_b);
+// Reference-mode CPU baseline (main.rs:159-290): `threads` workers, each
+// rendering whole 1-spp frames into a private buffer merged under a mutex,
+// for `passes_per_thread` passes. Returns wall seconds (< 0 on error).
+double orc_bench_reference_mode(orc_scene* s, uint32_t W, uint32_t H, uint32_t passes_per_thread, uint64_t seed,
+                                uint32_t max_depth, int threads, float* accum_rgb, uint32_t* accum_bounces,
+                                uint32_t row_begin, uint32_t row_end);
+void orc_get_counters(orc_scene* s, orc_counters* out);
+void orc_reset_counters(orc_scene* s);
+void orc_set_counting(orc_scene* s, int on);
+
+#ifdef __cplusplus
+}
+#endif
