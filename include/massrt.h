@@ -185,7 +185,8 @@ typedef struct {
   uint32_t shard_count; /* 0 or 1 = whole frame */
   uint32_t flags;       /* MRT_RENDER_* */
 } mrt_render_args;
-#define MRT_RENDER_COUNTERS 1u /* collect traversal counters (slower) */
+#define MRT_RENDER_COUNTERS 1u     /* collect traversal counters (slower) */
+#define MRT_RENDER_TIME_KERNELS 2u /* time every k_trace/k_shade launch with HIP events */
 
 /* Closest hit of one ray (parity entry point). */
 typedef struct {
@@ -209,6 +210,13 @@ typedef struct {
   uint64_t bounces;
 } mrt_counters;
 
+/* Kernel timing accumulated by renders flagged MRT_RENDER_TIME_KERNELS
+ * (HIP events on the stream the kernels run on). */
+typedef struct {
+  double trace_ms, shade_ms, other_ms;
+  uint64_t trace_launches, shade_launches, iterations;
+} mrt_kernel_stats;
+
 typedef struct mrt_ctx mrt_ctx;
 
 /* ---- device context ---------------------------------------------------- */
@@ -229,6 +237,8 @@ int mrt_render_device(mrt_ctx* ctx, const mrt_render_args* args, float* d_accum_
 int mrt_trace_rays(mrt_ctx* ctx, const float* rays, uint32_t n, float t_min, float t_max, mrt_hit* out);
 int mrt_get_counters(mrt_ctx* ctx, mrt_counters* out);
 int mrt_reset_counters(mrt_ctx* ctx);
+int mrt_get_kernel_stats(mrt_ctx* ctx, mrt_kernel_stats* out);
+int mrt_reset_kernel_stats(mrt_ctx* ctx);
 /* bytes of device memory held for the scene */
 int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
 

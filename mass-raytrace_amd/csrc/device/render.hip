@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <array>
 #include <map>
 #include <mutex>
 #include <string>
@@ -297,6 +298,10 @@ struct mrt_ctx {
   float* d_acc_rgb = nullptr;
   uint32_t* d_acc_b = nullptr;
   size_t acc_cap = 0;
+  // kernel timing
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  mrt_kernel_stats kstats{};
   // device ray buffer for mrt_trace_rays
   float* d_rays = nullptr;
   uint4* d_rhits = nullptr;
@@ -437,6 +442,16 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
     hipLaunchKernelGGL(k_generate, dim3((n0 + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c->cam, rp, c->bufs[0], n0);
     HIP_CHECK(hipGetLastError());
     const uint32_t grid = (uint32_t)((c->pool_cap + kBlock - 1) / kBlock);
+    const bool timing = (a->flags & MRT_RENDER_TIME_KERNELS) != 0;
+    std::vector<std::array<hipEvent_t, 3>> marks;
+    auto next_event = [&]() {
+      if (c->ev_used == c->ev_pool.size()) {
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreate(&e));
+        c->ev_pool.push_back(e);
+      }
+      return c->ev_pool[c->ev_used++];
+    };
     const int kBatch = 4;
     uint32_t it = 0;
     int slot = 0;
@@ -444,18 +459,34 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
     for (;;) {
       for (int b = 0; b < kBatch; ++b, ++it) {
         uint32_t cur = it & 1;
-        if (count) {
+        std::array<hipEvent_t, 3> m{};
+        if (timing) {
+          m[0] = next_event();
+          HIP_CHECK(hipEventRecord(m[0], st));
+        }
+        if (count)
           hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(kBlock), 0, st, c->S, c->bufs[cur], c->hits, c->ctrl,
                              cur, c->d_cnt);
-          hipLaunchKernelGGL(k_shade<true>, dim3(grid), dim3(kBlock), 0, st, c->S, c->cam, rp, c->bufs[cur],
-                             c->bufs[cur ^ 1], (const uint4*)c->hits, c->ctrl, cur, c->results, c->d_cnt);
-        } else {
+        else
           hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(kBlock), 0, st, c->S, c->bufs[cur], c->hits, c->ctrl,
                              cur, c->d_cnt);
+        HIP_CHECK(hipGetLastError());
+        if (timing) {
+          m[1] = next_event();
+          HIP_CHECK(hipEventRecord(m[1], st));
+        }
+        if (count)
+          hipLaunchKernelGGL(k_shade<true>, dim3(grid), dim3(kBlock), 0, st, c->S, c->cam, rp, c->bufs[cur],
+                             c->bufs[cur ^ 1], (const uint4*)c->hits, c->ctrl, cur, c->results, c->d_cnt);
+        else
           hipLaunchKernelGGL(k_shade<false>, dim3(grid), dim3(kBlock), 0, st, c->S, c->cam, rp, c->bufs[cur],
                              c->bufs[cur ^ 1], (const uint4*)c->hits, c->ctrl, cur, c->results, c->d_cnt);
-        }
         HIP_CHECK(hipGetLastError());
+        if (timing) {
+          m[2] = next_event();
+          HIP_CHECK(hipEventRecord(m[2], st));
+          marks.push_back(m);
+        }
       }
       HIP_CHECK(hipMemcpyAsync(&c->h_status[slot], c->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, st));
       HIP_CHECK(hipEventRecord(c->ev[slot], st));
@@ -468,6 +499,20 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
       pending = true;
       slot ^= 1;
       if (it > 64u * 1024u) throw ApiError{MRT_ERR_HIP, "render did not converge"};
+    }
+    if (timing) {
+      HIP_CHECK(hipStreamSynchronize(st));
+      for (auto& m : marks) {
+        float t0 = 0, t1 = 0;
+        HIP_CHECK(hipEventElapsedTime(&t0, m[0], m[1]));
+        HIP_CHECK(hipEventElapsedTime(&t1, m[1], m[2]));
+        c->kstats.trace_ms += t0;
+        c->kstats.shade_ms += t1;
+        c->kstats.trace_launches++;
+        c->kstats.shade_launches++;
+        c->kstats.iterations++;
+      }
+      c->ev_used = 0;
     }
     hipLaunchKernelGGL(k_accumulate, dim3((n_pix + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
                        (const float4*)c->results, n_pix, cs, (const uint32_t*)pl.first, d_rgb, d_b);
@@ -538,6 +583,7 @@ int mrt_destroy(mrt_ctx* c) {
   if (c->h_status) hipHostFree(c->h_status);
   if (c->ev[0]) hipEventDestroy(c->ev[0]);
   if (c->ev[1]) hipEventDestroy(c->ev[1]);
+  for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
   return MRT_OK;
@@ -704,6 +750,17 @@ int mrt_get_counters(mrt_ctx* c, mrt_counters* out) {
     out->texel_taps = h.texel_taps;
     out->bounces = h.bounces;
   });
+}
+
+int mrt_get_kernel_stats(mrt_ctx* c, mrt_kernel_stats* out) {
+  return guarded(c, [&] {
+    if (!out) throw ApiError{MRT_ERR_INVALID, "null output"};
+    *out = c->kstats;
+  });
+}
+
+int mrt_reset_kernel_stats(mrt_ctx* c) {
+  return guarded(c, [&] { c->kstats = mrt_kernel_stats{}; });
 }
 
 int mrt_reset_counters(mrt_ctx* c) {

@@ -79,7 +79,8 @@ struct Emitter {
 
   // Triangle::intersect runs alpha_test only with uvs; it can reject only if
   // the triangle's own material samples a texture holding a zero alpha.
-  bool needs_alpha(const mrt_triangle& t) const {
+  std::vector<int8_t> tex_zero_alpha;  // per texture, computed once
+  bool needs_alpha(const mrt_triangle& t) {
     if (!(t.flags & MRT_TRI_HAS_UV) || t.material >= d.n_materials) return false;
     const mrt_material& m = d.materials[t.material];
     if (m.kind != MRT_MAT_LAMBERTIAN && m.kind != MRT_MAT_METAL) return false;
@@ -87,10 +88,18 @@ struct Emitter {
     const mrt_surface& sf = d.surfaces[m.surface];
     if (sf.kind == MRT_SURF_SOLID) return sf.color[3] == 0.0f;
     if (sf.texture >= d.n_textures) return false;
-    const mrt_texture& tx = d.textures[sf.texture];
-    for (size_t i = 0; i < (size_t)tx.width * tx.height; ++i)
-      if (tx.rgba[4 * i + 3] == 0) return true;
-    return false;
+    if (tex_zero_alpha.empty()) tex_zero_alpha.assign(d.n_textures, -1);
+    int8_t& z = tex_zero_alpha[sf.texture];
+    if (z < 0) {
+      const mrt_texture& tx = d.textures[sf.texture];
+      z = 0;
+      for (size_t i = 0; i < (size_t)tx.width * tx.height; ++i)
+        if (tx.rgba[4 * i + 3] == 0) {
+          z = 1;
+          break;
+        }
+    }
+    return z == 1;
   }
 
   bool fail(const char* m) {
@@ -145,7 +154,7 @@ void put_m4_12(std::vector<float>& dst, const float* m16) {
 
 bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
   s = HostScene{};
-  Emitter e{d, s, err, {}};
+  Emitter e{d, s, err, {}, {}};
   // materials
   for (uint32_t i = 0; i < d.n_materials; ++i) {
     const mrt_material& m = d.materials[i];

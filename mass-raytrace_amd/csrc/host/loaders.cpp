@@ -9,6 +9,7 @@
 #include <string.h>
 #include <zlib.h>
 
+#include <algorithm>
 #include <array>
 #include <fstream>
 #include <sstream>
@@ -461,16 +462,14 @@ bool decode_png(const std::string& path, std::vector<uint8_t>& rgba, uint32_t& w
     }
     p += 12 + len;
   }
-  if (depth != 8 || interlace != 0) {
-    err = "only 8-bit non-interlaced PNG is supported";
-    return false;
-  }
   int ch = ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 3 ? 1 : ctype == 4 ? 2 : ctype == 6 ? 4 : 0;
-  if (!ch) {
-    err = "bad PNG color type";
+  bool sub_byte_ok = (ctype == 0 || ctype == 3) && (depth == 1 || depth == 2 || depth == 4);
+  if (!ch || interlace != 0 || !(depth == 8 || sub_byte_ok)) {
+    err = "unsupported PNG (need 8-bit, or 1/2/4-bit gray/palette; non-interlaced)";
     return false;
   }
-  size_t stride = (size_t)w * ch;
+  const size_t stride = ((size_t)w * ch * depth + 7) / 8;
+  const size_t bpp = std::max<size_t>(1, (size_t)ch * depth / 8);
   std::vector<unsigned char> raw((stride + 1) * h);
   uLongf rawlen = raw.size();
   if (uncompress(raw.data(), &rawlen, idat.data(), idat.size()) != Z_OK || rawlen != raw.size()) {
@@ -483,7 +482,7 @@ bool decode_png(const std::string& path, std::vector<uint8_t>& rgba, uint32_t& w
     unsigned char* src = &raw[y * (stride + 1) + 1];
     unsigned char* dst = &img[y * stride];
     for (size_t x = 0; x < stride; ++x) {
-      int a = x >= (size_t)ch ? dst[x - ch] : 0, b = prev[x], cc = x >= (size_t)ch ? prev[x - ch] : 0;
+      int a = x >= bpp ? dst[x - bpp] : 0, b = prev[x], cc = x >= bpp ? prev[x - bpp] : 0;
       int pred = 0;
       if (f == 1) pred = a;
       else if (f == 2) pred = b;
@@ -499,33 +498,46 @@ bool decode_png(const std::string& path, std::vector<uint8_t>& rgba, uint32_t& w
     }
     memcpy(prev.data(), dst, stride);
   }
+  auto sample = [&](uint32_t y, size_t i) -> unsigned {  // i-th sample of row y
+    if (depth == 8) return img[y * stride + i];
+    size_t bit = i * depth;
+    unsigned byte = img[y * stride + bit / 8];
+    return (byte >> (8 - depth - bit % 8)) & ((1u << depth) - 1);
+  };
+  const unsigned maxv = (1u << depth) - 1;
   rgba.resize((size_t)w * h * 4);
-  for (size_t i = 0; i < (size_t)w * h; ++i) {
-    unsigned char* o = &rgba[4 * i];
-    const unsigned char* s = &img[i * ch];
-    switch (ctype) {
-      case 0:
-        o[0] = o[1] = o[2] = s[0], o[3] = 255;
-        break;
-      case 2:
-        o[0] = s[0], o[1] = s[1], o[2] = s[2], o[3] = 255;
-        break;
-      case 3: {
-        size_t k = s[0];
-        if (3 * k + 2 >= plte.size()) {
-          err = "PNG palette index out of range";
-          return false;
+  for (uint32_t y = 0; y < h; ++y)
+    for (uint32_t x = 0; x < w; ++x) {
+      unsigned char* o = &rgba[4 * ((size_t)y * w + x)];
+      size_t i0 = (size_t)x * ch;
+      switch (ctype) {
+        case 0: {
+          unsigned v = sample(y, i0);
+          o[0] = o[1] = o[2] = (unsigned char)(v * 255 / maxv);
+          o[3] = (trns.size() >= 2 && v == (unsigned)(trns[0] << 8 | trns[1])) ? 0 : 255;
+          break;
         }
-        o[0] = plte[3 * k], o[1] = plte[3 * k + 1], o[2] = plte[3 * k + 2], o[3] = k < trns.size() ? trns[k] : 255;
-        break;
+        case 2:
+          o[0] = (unsigned char)sample(y, i0), o[1] = (unsigned char)sample(y, i0 + 1),
+          o[2] = (unsigned char)sample(y, i0 + 2);
+          o[3] = (trns.size() >= 6 && o[0] == trns[1] && o[1] == trns[3] && o[2] == trns[5]) ? 0 : 255;
+          break;
+        case 3: {
+          size_t k = sample(y, i0);
+          if (3 * k + 2 >= plte.size()) {
+            err = "PNG palette index out of range";
+            return false;
+          }
+          o[0] = plte[3 * k], o[1] = plte[3 * k + 1], o[2] = plte[3 * k + 2], o[3] = k < trns.size() ? trns[k] : 255;
+          break;
+        }
+        case 4:
+          o[0] = o[1] = o[2] = (unsigned char)sample(y, i0), o[3] = (unsigned char)sample(y, i0 + 1);
+          break;
+        default:
+          for (int k = 0; k < 4; ++k) o[k] = (unsigned char)sample(y, i0 + k);
       }
-      case 4:
-        o[0] = o[1] = o[2] = s[0], o[3] = s[1];
-        break;
-      default:
-        memcpy(o, s, 4);
     }
-  }
   return true;
 }
 

@@ -28,6 +28,7 @@ WRAP_MIRROR, WRAP_REPEAT, WRAP_CLAMP = range(3)
 BG_SOLID, BG_SKY, BG_SKYSPHERE = range(3)
 NO_MATERIAL = 0xFFFFFFFF
 RENDER_COUNTERS = 1
+RENDER_TIME_KERNELS = 2
 MAX_DEPTH = 50  # main.rs:37
 ASPECT_RATIO = np.float32(16.0) / np.float32(9.0)  # main.rs:39 (f32)
 
@@ -124,6 +125,14 @@ COUNTER_FIELDS = ["samples", "segments", "node_visits", "sphere_tests", "triangl
                   "model_entries", "closest_hits", "texel_taps", "bounces"]
 
 
+class MrtKernelStats(C.Structure):
+    _fields_ = [("trace_ms", C.c_double), ("shade_ms", C.c_double), ("other_ms", C.c_double),
+                ("trace_launches", C.c_uint64), ("shade_launches", C.c_uint64), ("iterations", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
 class MrtCounters(C.Structure):
     _fields_ = [(f, C.c_uint64) for f in COUNTER_FIELDS]
 
@@ -135,7 +144,8 @@ class MrtCounters(C.Structure):
 EXPORTED_SYMBOLS = [
     "mrt_create", "mrt_destroy", "mrt_last_error", "mrt_global_last_error", "mrt_abi_version",
     "mrt_upload_scene", "mrt_set_camera", "mrt_render", "mrt_render_device", "mrt_trace_rays",
-    "mrt_get_counters", "mrt_reset_counters", "mrt_scene_device_bytes",
+    "mrt_get_counters", "mrt_reset_counters", "mrt_scene_device_bytes", "mrt_get_kernel_stats",
+    "mrt_reset_kernel_stats",
     "mrt_builder_new", "mrt_builder_free", "mrt_builder_builtin", "mrt_builder_rand_f32", "mrt_builder_solid",
     "mrt_builder_texture_png", "mrt_builder_texture_rgba", "mrt_builder_material", "mrt_builder_background",
     "mrt_builder_add_sphere", "mrt_builder_add_triangle", "mrt_builder_model", "mrt_builder_model_from_ply",
@@ -170,6 +180,8 @@ def lib() -> C.CDLL:
         "mrt_trace_rays": (I, [P, fp, U32, F, F, C.POINTER(MrtHit)]),
         "mrt_get_counters": (I, [P, C.POINTER(MrtCounters)]),
         "mrt_reset_counters": (I, [P]),
+        "mrt_get_kernel_stats": (I, [P, C.POINTER(MrtKernelStats)]),
+        "mrt_reset_kernel_stats": (I, [P]),
         "mrt_scene_device_bytes": (I, [P, C.POINTER(C.c_uint64)]),
         "mrt_builder_new": (I, [U64, C.POINTER(P)]),
         "mrt_builder_free": (I, [P]),
@@ -385,9 +397,9 @@ class Context:
 
     @staticmethod
     def args(width, height, spp_begin=0, spp_count=1, seed=1, max_depth=MAX_DEPTH, shard_index=0, shard_count=1,
-             counters=False) -> MrtRenderArgs:
-        return MrtRenderArgs(width, height, spp_begin, spp_count, seed, max_depth, shard_index, shard_count,
-                             RENDER_COUNTERS if counters else 0)
+             counters=False, time_kernels=False) -> MrtRenderArgs:
+        flags = (RENDER_COUNTERS if counters else 0) | (RENDER_TIME_KERNELS if time_kernels else 0)
+        return MrtRenderArgs(width, height, spp_begin, spp_count, seed, max_depth, shard_index, shard_count, flags)
 
     def render(self, width, height, spp_begin=0, spp_count=1, seed=1, max_depth=MAX_DEPTH, shard_index=0,
                shard_count=1, counters=False, accum=None):
@@ -420,6 +432,14 @@ class Context:
 
     def reset_counters(self):
         self._check(lib().mrt_reset_counters(self.h))
+
+    def kernel_stats(self) -> dict:
+        k = MrtKernelStats()
+        self._check(lib().mrt_get_kernel_stats(self.h, C.byref(k)))
+        return k.as_dict()
+
+    def reset_kernel_stats(self):
+        self._check(lib().mrt_reset_kernel_stats(self.h))
 
 
 def load_ply(path) -> np.ndarray:

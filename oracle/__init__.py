@@ -61,6 +61,8 @@ def lib() -> C.CDLL:
         "orc_render_pixels": (I, [P, U32, U32, up, U32, U32, U32, U64, U32, I, fp, up]),
         "orc_bench_reference_mode": (C.c_double, [P, U32, U32, U32, U64, U32, I, fp, up, U32, U32]),
         "orc_get_counters": (None, [P, P]),
+        "orc_wyrand": (None, [U64, U32, C.POINTER(C.c_uint64), fp]),
+        "orc_path_rng": (None, [U64, U32, U32, U32, C.POINTER(C.c_uint64), fp]),
         "orc_reset_counters": (None, [P]),
         "orc_set_counting": (None, [P, I]),
     }
@@ -90,6 +92,20 @@ def _up(a):
 
 def _f3(v):
     return np.ascontiguousarray(np.asarray(v, dtype=np.float32).reshape(3))
+
+
+def wyrand(seed: int, n: int):
+    u = np.zeros(n, dtype=np.uint64)
+    f = np.zeros(n, dtype=np.float32)
+    lib().orc_wyrand(seed, n, u.ctypes.data_as(C.POINTER(C.c_uint64)), _fp(f))
+    return u, f
+
+
+def path_rng(seed: int, pixel: int, sample: int, n: int):
+    u = np.zeros(n, dtype=np.uint64)
+    f = np.zeros(n, dtype=np.float32)
+    lib().orc_path_rng(seed, pixel, sample, n, u.ctypes.data_as(C.POINTER(C.c_uint64)), _fp(f))
+    return u, f
 
 
 class OracleError(RuntimeError):

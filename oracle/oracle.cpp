@@ -564,8 +564,15 @@ struct BvhNode : Intersect {  // geom.rs:103-205
         left = std::move(b), right = std::move(a);
       }
     } else {
-      std::stable_sort(items.begin(), items.end(),
-                       [axis](const Obj& x, const Obj& y) { return cmp_key(x.get(), axis) < cmp_key(y.get(), axis); });
+      // sort_by(|a, b| compare(a, b)): stable, only is_less consulted; keys
+      // are read once per item (bounding_box() is a pure function here)
+      std::vector<std::pair<float, size_t>> keys(items.size());
+      for (size_t i = 0; i < items.size(); ++i) keys[i] = {cmp_key(items[i].get(), axis), i};
+      std::stable_sort(keys.begin(), keys.end(),
+                       [](const std::pair<float, size_t>& x, const std::pair<float, size_t>& y) { return x.first < y.first; });
+      std::vector<Obj> sorted(items.size());
+      for (size_t i = 0; i < keys.size(); ++i) sorted[i] = std::move(items[keys[i].second]);
+      items = std::move(sorted);
       size_t mid = items.size() / 2;
       std::vector<Obj> back;
       for (size_t i = mid; i < items.size(); ++i) back.push_back(std::move(items[i]));
@@ -1511,6 +1518,16 @@ double orc_bench_reference_mode(orc_scene* s, uint32_t W, uint32_t H, uint32_t p
   for (auto& t : ts) t.join();
   double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return failed ? -1.0 : secs;
+}
+
+// RNG streams exposed for known-answer tests
+void orc_wyrand(uint64_t seed, uint32_t n, uint64_t* out_u64, float* out_f32) {
+  Wy a{seed}, b{seed};
+  for (uint32_t i = 0; i < n; ++i) out_u64[i] = a.u64(), out_f32[i] = b.f32();
+}
+void orc_path_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint64_t* out_u64, float* out_f32) {
+  PathRng a(seed, pixel, sample), b(seed, pixel, sample);
+  for (uint32_t i = 0; i < n; ++i) out_u64[i] = a.next(), out_f32[i] = b.f32();
 }
 
 void orc_get_counters(orc_scene* s, orc_counters* o) {

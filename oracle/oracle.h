@@ -84,6 +84,8 @@ int orc_render_pixels(orc_scene* s, uint32_t W, uint32_t H, const uint32_t* pixe
 double orc_bench_reference_mode(orc_scene* s, uint32_t W, uint32_t H, uint32_t passes_per_thread, uint64_t seed,
                                 uint32_t max_depth, int threads, float* accum_rgb, uint32_t* accum_bounces,
                                 uint32_t row_begin, uint32_t row_end);
+void orc_wyrand(uint64_t seed, uint32_t n, uint64_t* out_u64, float* out_f32);
+void orc_path_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint64_t* out_u64, float* out_f32);
 void orc_get_counters(orc_scene* s, orc_counters* out);
 void orc_reset_counters(orc_scene* s);
 void orc_set_counting(orc_scene* s, int on);

@@ -1,0 +1,129 @@
+"""BVH topology: the host builder (product) and the oracle must build the
+reference's tree (BvhNode::new, geom.rs:110-161: one fastrand::u8(0..3)
+draw per call, stable sort on bbox.min[axis], median split, n=2 pop order)
+node for node, box for box."""
+import numpy as np
+import pytest
+
+import massrt
+import oracle
+
+
+def T(n):
+    # node count of BvhNode::new over n items: T(1)=T(2)=1, T(n)=1+T(n//2)+T(n-n//2)
+    memo = {1: 1, 2: 1}
+
+    def t(k):
+        if k not in memo:
+            memo[k] = 1 + t(k // 2) + t(k - k // 2)
+        return memo[k]
+    return t(n)
+
+
+def assert_same_tree(b: massrt.Builder, o: oracle.Scene):
+    d = b.desc_only()
+    lst, boxes = massrt.preorder(d)
+    k, bx = o.preorder()
+    assert [tuple(x) for x in k.tolist()] == lst
+    pb = np.array([x for x in boxes if x is not None], dtype=np.float32).reshape(-1, 6)
+    ob = bx[k[:, 0] == 1]
+    assert np.array_equal(pb.view(np.uint32), ob.view(np.uint32))
+    # every BLAS (Model::new trees) too
+    for m in range(o.blas_count()):
+        kb, bb = o.blas_preorder(m)
+        assert kb[0, 0] == 1
+    return d
+
+
+def test_node_count_formula():
+    assert T(12) == 15 and T(10_001) == 11_809 and T(1_000_000) == 1_048_575
+
+
+@pytest.mark.parametrize("name", ["cornell", "sphere_grid", "cube_field"])
+def test_builtin_scene_topology(name, golden_dir):
+    aspect = float(massrt.ASPECT_RATIO)
+    b = massrt.Builder(1).builtin(name, aspect, golden_dir)
+    o = oracle.Scene(1).builtin(name, aspect, golden_dir)
+    d = assert_same_tree(b, o)
+    cam, _ = b.desc()[1], None
+    assert np.array_equal(cam.fields().view(np.uint32), o.camera_fields().view(np.uint32))
+    if name == "sphere_grid":
+        assert d.n_nodes == T(10_001) + T(12)
+        assert d.n_spheres == 10_000 and d.n_instances == 1
+
+
+@pytest.mark.parametrize("name", ["mesh_ply", "mesh_obj", "mesh_obj_textured"])
+def test_mesh_scene_topology(name, assets_dir):
+    aspect = float(massrt.ASPECT_RATIO)
+    b = massrt.Builder(1).builtin(name, aspect, assets_dir)
+    o = oracle.Scene(1).builtin(name, aspect, assets_dir)
+    d = b.desc_only()
+    assert d.n_triangles == 1_000_000 + 12
+    lst, _ = massrt.preorder(d)
+    k, _ = o.preorder()
+    assert [tuple(x) for x in k.tolist()] == lst
+    # the 1M-triangle BLAS, node for node and box for box
+    m = d.models[0]
+    sub = massrt.MrtSceneDesc()
+    sub.nodes = d.nodes
+    sub.roots = (massrt.C.c_uint32 * 1)((massrt.REF_NODE << 28) | m.blas_root)
+    sub.n_roots = 1
+    l2, b2 = massrt.preorder(sub)
+    kb, bb = o.blas_preorder(1)
+    assert [tuple(x) for x in kb.tolist()] == l2
+    pb = np.array([x for x in b2 if x is not None], dtype=np.float32)
+    assert np.array_equal(pb.view(np.uint32), bb[kb[:, 0] == 1].view(np.uint32))
+    assert sum(1 for x in l2 if x[0] == 1) == T(1_000_000)
+
+
+def random_world(seed, n_spheres, ties):
+    """Same random world built through both builders."""
+    rng = np.random.default_rng(seed)
+    b, o = massrt.Builder(seed), oracle.Scene(seed)
+    sb, so = b.solid(0.5, 0.5, 0.5), o.solid(0.5, 0.5, 0.5)
+    mb, mo = b.material(massrt.MAT_LAMBERTIAN, sb), o.material(1, so)
+    cube = np.array([[1, 1, 1, -1, 1, -1, -1, 1, 1], [1, -1, -1, -1, -1, -1, 1, 1, -1]], dtype=np.float32)
+    kb = b.model(mb, cube)
+    ko = o.model(mo, cube)
+    for i in range(n_spheres):
+        c = rng.integers(-3, 3, size=3).astype(np.float32) if ties else rng.normal(size=3).astype(np.float32) * 5
+        r = float(rng.choice([0.5, 1.0, -0.5])) if ties else float(rng.uniform(0.1, 1))
+        b.add_sphere(mb, c, r)
+        o.add_sphere(mo, c, r)
+        if i % 7 == 0:
+            t, rot, s = rng.normal(size=3), rng.normal(size=3), rng.uniform(0.5, 2, size=3)
+            b.add_instance(kb, t, rot, s, mb)
+            o.add_instance(ko, t, rot, s, mo)
+        if i % 11 == 0:
+            tri = rng.integers(-2, 2, size=9).astype(np.float32) if ties else rng.normal(size=9).astype(np.float32)
+            b.add_triangle(mb, tri)
+            o.add_triangle(mo, tri)
+    b.build_bvh()
+    o.build_bvh()
+    return b, o
+
+
+@pytest.mark.parametrize("seed,n,ties", [(1, 1, False), (2, 2, False), (3, 3, True), (4, 64, True),
+                                         (5, 333, False), (6, 1000, True)])
+def test_random_worlds_same_tree(seed, n, ties):
+    b, o = random_world(seed, n, ties)
+    assert_same_tree(b, o)
+    assert b.rand_f32() == o.rand_f32()  # same number of scene-stream draws
+
+
+def test_two_items_pop_order():
+    # n == 2: a = items.pop() (last) goes left only if a.min < b.min (geom.rs:122-129)
+    for order in [(0.0, 5.0), (5.0, 0.0), (2.0, 2.0)]:
+        b, o = massrt.Builder(9), oracle.Scene(9)
+        s = b.solid(1, 1, 1)
+        m = b.material(massrt.MAT_LAMBERTIAN, s)
+        om = o.material(1, o.solid(1, 1, 1))
+        for x in order:
+            b.add_sphere(m, (x, x, x), 1.0)
+            o.add_sphere(om, (x, x, x), 1.0)
+        b.build_bvh()
+        o.build_bvh()
+        lst, _ = massrt.preorder(b.desc_only())
+        first = lst[1][1]
+        assert first == (1 if order[1] < order[0] else 0)
+        assert_same_tree(b, o)

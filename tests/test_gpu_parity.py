@@ -1,0 +1,253 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the oracle.
+
+Bar (BASELINE.json north_star): closest-hit ids / t / front_face, bounce
+counts and traversal counters bit-exact; radiance within 1e-4 relative L2
+(RTOL below). The GPU folds radiance forward (T *= atten) where the reference
+recursion folds it post-order (world.rs:71-72), so radiance differs by ULPs."""
+import numpy as np
+import pytest
+
+import massrt
+import oracle
+
+pytestmark = pytest.mark.gpu
+ASPECT = float(massrt.ASPECT_RATIO)
+RTOL = 1e-4  # relative L2 on accumulated radiance (north_star)
+SMALL = ["cornell", "sphere_grid", "cube_field"]
+MESH = ["mesh_ply", "mesh_obj", "mesh_obj_textured"]
+
+
+def rel_l2(a, b):
+    return float(np.linalg.norm(a.astype(np.float64) - b) / max(np.linalg.norm(b.astype(np.float64)), 1e-30))
+
+
+def random_rays(n, seed, span=15.0):
+    rng = np.random.default_rng(seed)
+    o = rng.uniform(-span, span, (n, 3)).astype(np.float32)
+    o[:, 1] = np.abs(o[:, 1]) + 0.5
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    return np.concatenate([o, d], 1)
+
+
+def camera_rays(cam, n, seed):
+    """Primary rays in the camera frustum (Camera::ray with jitter, world.rs:53-63)."""
+    rng = np.random.default_rng(seed)
+    f = cam.fields()
+    org, llc, hor, ver = f[0:3], f[3:6], f[6:9], f[9:12]
+    s = rng.random(n, dtype=np.float32)[:, None]
+    t = rng.random(n, dtype=np.float32)[:, None]
+    d = (((llc + hor * s) + ver * t) - org).astype(np.float32)
+    return np.concatenate([np.broadcast_to(org, (n, 3)), d], 1).astype(np.float32)
+
+
+@pytest.fixture(scope="module")
+def small_scenes(golden_dir):
+    out = {}
+    for s in SMALL:
+        out[s] = (massrt.Builder(1).builtin(s, ASPECT, golden_dir), oracle.Scene(1).builtin(s, ASPECT, golden_dir))
+    return out
+
+
+@pytest.mark.parametrize("scene", SMALL)
+def test_golden_rays_bit_exact(ctx, small_scenes, golden_dir, scene):
+    g = np.load(golden_dir / "oracle_golden.npz")
+    b, _ = small_scenes[scene]
+    ctx.upload(b)
+    assert np.array_equal(ctx.trace_rays(g["rays"]), g[f"{scene}_hits"])
+
+
+@pytest.mark.parametrize("scene", SMALL)
+def test_trace_rays_bit_exact(ctx, small_scenes, scene):
+    b, o = small_scenes[scene]
+    ctx.upload(b)
+    _, cam = b.desc()
+    for rays in (random_rays(40_000, 1), camera_rays(cam, 40_000, 2)):
+        ctx.reset_counters()
+        o.reset_counters()
+        gh, oh = ctx.trace_rays(rays), o.trace_rays(rays)
+        assert np.array_equal(gh, oh), f"{int((gh != oh).any(1).sum())} rays differ"
+        gc, oc = ctx.counters(), o.counters()
+        for k in ["segments", "node_visits", "sphere_tests", "triangle_tests", "instance_entries", "closest_hits"]:
+            assert gc[k] == oc[k], k
+
+
+@pytest.mark.parametrize("scene", SMALL)
+def test_golden_render(ctx, small_scenes, golden_dir, scene):
+    g = np.load(golden_dir / "oracle_golden.npz")
+    b, _ = small_scenes[scene]
+    ctx.upload(b)
+    rgb, bo = ctx.render(32, 18, 0, 2, seed=3)
+    assert np.array_equal(bo, g[f"{scene}_bounces"])
+    assert rel_l2(rgb, g[f"{scene}_rgb"]) <= RTOL
+
+
+@pytest.mark.parametrize("scene", SMALL)
+def test_render_parity_and_counters(ctx, small_scenes, scene):
+    b, o = small_scenes[scene]
+    ctx.upload(b)
+    W, H, spp = 96, 54, 4
+    ctx.reset_counters()
+    o.reset_counters()
+    rgb, bo = ctx.render(W, H, 0, spp, seed=17, counters=True)
+    orgb, obo = o.render(W, H, 0, spp, seed=17, threads=0)
+    assert np.array_equal(bo, obo)
+    assert rel_l2(rgb, orgb) <= RTOL
+    gc, oc = ctx.counters(), o.counters()
+    for k in massrt.COUNTER_FIELDS:
+        assert gc[k] == oc[k], (k, gc[k], oc[k])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("scene", MESH)
+def test_mesh_scene_parity(ctx, assets_dir, scene):
+    b = massrt.Builder(1).builtin(scene, ASPECT, assets_dir)
+    o = oracle.Scene(1).builtin(scene, ASPECT, assets_dir)
+    ctx.upload(b)
+    _, cam = b.desc()
+    rays = camera_rays(cam, 20_000, 5)
+    assert np.array_equal(ctx.trace_rays(rays), o.trace_rays(rays))
+    W, H, spp = 48, 27, 2
+    ctx.reset_counters()
+    o.reset_counters()
+    rgb, bo = ctx.render(W, H, 0, spp, seed=23, counters=True)
+    orgb, obo = o.render(W, H, 0, spp, seed=23)
+    assert np.array_equal(bo, obo)
+    assert rel_l2(rgb, orgb) <= RTOL
+    gc, oc = ctx.counters(), o.counters()
+    for k in ["samples", "segments", "node_visits", "triangle_tests", "instance_entries", "model_entries",
+              "closest_hits", "bounces", "texel_taps"]:
+        assert gc[k] == oc[k], (k, gc[k], oc[k])
+
+
+def test_render_additive_and_shard_invariant(ctx, small_scenes):
+    b, _ = small_scenes["sphere_grid"]
+    ctx.upload(b)
+    W, H = 70, 41
+    full = ctx.render(W, H, 0, 4, seed=5)
+    half = ctx.render(W, H, 0, 2, seed=5)
+    half = ctx.render(W, H, 2, 2, seed=5, accum=half)
+    assert np.array_equal(full[0].view(np.uint32), half[0].view(np.uint32)) and np.array_equal(full[1], half[1])
+    acc = (np.zeros(W * H * 3, np.float32), np.zeros(W * H, np.uint32))
+    for i in range(3):
+        acc = ctx.render(W, H, 0, 4, seed=5, shard_index=i, shard_count=3, accum=acc)
+    assert np.array_equal(full[0].view(np.uint32), acc[0].view(np.uint32)) and np.array_equal(full[1], acc[1])
+    again = ctx.render(W, H, 0, 4, seed=5)
+    assert np.array_equal(full[0].view(np.uint32), again[0].view(np.uint32))
+
+
+def test_depth_limits(ctx, small_scenes):
+    b, o = small_scenes["cornell"]
+    ctx.upload(b)
+    rgb, bo = ctx.render(16, 9, 0, 2, seed=1, max_depth=0)
+    assert not rgb.any() and not bo.any()
+    for depth in (1, 2, 3):
+        g = ctx.render(40, 22, 0, 2, seed=1, max_depth=depth)
+        r = o.render(40, 22, 0, 2, seed=1, max_depth=depth)
+        assert np.array_equal(g[1], r[1]) and rel_l2(g[0], r[0]) <= RTOL
+        assert g[1].max() <= 2 * depth
+
+
+def build_both(fn):
+    b, o = massrt.Builder(3), oracle.Scene(3)
+    fn(b)
+    fn(o)
+    return b, o
+
+
+@pytest.mark.parametrize("kind,param", [(massrt.MAT_LAMBERTIAN, 0.0), (massrt.MAT_METAL, 0.0),
+                                        (massrt.MAT_DIELECTRIC, 1.5)])
+def test_furnace_exact_on_gpu(ctx, kind, param):
+    def scene(x):
+        x.background(massrt.BG_SOLID, 0, (1.0, 1.0, 1.0))
+        m = x.material(kind, x.solid(1, 1, 1, 1), param)
+        x.add_sphere(m, (0, 0, 0), 1.0)
+        x.build_bvh()
+        x.camera(40.0, (0, 0, 4), (0, 0, 0), aspect=ASPECT)
+    b, o = build_both(scene)
+    ctx.upload(b)
+    rgb, bo = ctx.render(24, 16, 0, 8, seed=5)
+    orgb, obo = o.render(24, 16, 0, 8, seed=5)
+    assert np.array_equal(bo, obo)
+    assert np.array_equal(rgb, orgb)  # exact: products of 1.0
+    assert np.all(rgb == np.round(rgb))
+
+
+def test_backgrounds_textures_and_alpha(ctx):
+    """SkyBackground / SkySphere (acos/atan2 differ by ULPs between ocml and
+    glibc: radiance only), textured Lambertian with uvs, and the alpha test
+    inside Triangle::intersect (geom.rs:567-571) on a cut-out texture."""
+    rng = np.random.default_rng(7)
+    tex = rng.integers(0, 256, size=(16, 24, 4), dtype=np.uint8)
+    tex[..., 3] = np.where(rng.random((16, 24)) < 0.3, 0, 255)
+    env = rng.integers(0, 256, size=(32, 64, 4), dtype=np.uint8)
+    grid = np.linspace(-2, 2, 9, dtype=np.float32)
+    tris = []
+    for i in range(8):
+        for j in range(8):
+            x0, x1, y0, y1 = grid[i], grid[i + 1], grid[j], grid[j + 1]
+            n = [0, 0, 1]
+            c = [[x0, y0, 0], [x1, y0, 0], [x1, y1, 0]], [[x0, y0, 0], [x1, y1, 0], [x0, y1, 0]]
+            for tri in c:
+                row = []
+                for v in tri:
+                    row += list(v) + n + [v[0] * 0.3 + 0.5, v[1] * 0.3 + 0.5]
+                tris.append(row)
+    tris = np.array(tris, dtype=np.float32)
+    for bg in (massrt.BG_SKY, massrt.BG_SKYSPHERE):
+        def scene(x, bg=bg):
+            st = x.texture_rgba(tex, massrt.WRAP_REPEAT)
+            se = x.texture_rgba(env, massrt.WRAP_CLAMP)
+            if bg == massrt.BG_SKY:
+                x.background(bg)
+            else:
+                x.background(bg, se)
+            mt = x.material(massrt.MAT_LAMBERTIAN, st)
+            mm = x.material(massrt.MAT_METAL, st, 0.3)
+            m = x.model(mt, tris, add_to_world=True, shading=True)
+            x.add_instance(m, (0.5, 0.2, -1.5), (0.1, 0.2, 0.05), (1.2, 0.8, 1.0), mm)
+            x.add_sphere(x.material(massrt.MAT_DIELECTRIC, 0, 1.4), (0.3, 0.1, 1.0), 0.5)
+            x.build_bvh()
+            x.camera(45.0, (0.5, 0.8, 6), (0, 0, 0), aspect=ASPECT)
+        b, o = build_both(scene)
+        ctx.upload(b)
+        _, cam = b.desc()
+        rays = camera_rays(cam, 20_000, 9)
+        assert np.array_equal(ctx.trace_rays(rays), o.trace_rays(rays))
+        ctx.reset_counters()
+        o.reset_counters()
+        rgb, bo = ctx.render(64, 36, 0, 4, seed=8, counters=True)
+        orgb, obo = o.render(64, 36, 0, 4, seed=8)
+        assert np.array_equal(bo, obo)
+        assert rel_l2(rgb, orgb) <= RTOL
+        gc, oc = ctx.counters(), o.counters()
+        assert gc["model_entries"] == oc["model_entries"] > 0
+        assert oc["alpha_taps"] > 0
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_worlds_with_ties(ctx, seed):
+    from test_bvh import random_world
+    b, o = random_world(seed + 10, 400, ties=True)
+    b.camera(50.0, (8, 6, 9), (0, 0, 0), aspect=ASPECT)
+    o.camera(50.0, (8, 6, 9), (0, 0, 0), aspect=ASPECT)
+    ctx.upload(b)
+    rays = random_rays(30_000, seed, span=4.0)
+    assert np.array_equal(ctx.trace_rays(rays), o.trace_rays(rays))
+    rgb, bo = ctx.render(40, 30, 0, 3, seed=seed)
+    orgb, obo = o.render(40, 30, 0, 3, seed=seed)
+    assert np.array_equal(bo, obo) and rel_l2(rgb, orgb) <= RTOL
+
+
+def test_errors_are_reported(ctx):
+    import ctypes as C
+    fresh = massrt.Context(0)
+    with pytest.raises(massrt.MassrtError, match="no scene"):
+        fresh.render(8, 8, 0, 1)
+    b = massrt.Builder(1)
+    s = b.texture_rgba(np.zeros((2, 2, 4), np.uint8), massrt.WRAP_MIRROR)
+    b.add_sphere(b.material(massrt.MAT_LAMBERTIAN, s), (0, 0, 0), 1)
+    b.build_bvh()
+    d = b.desc_only()
+    with pytest.raises(massrt.MassrtError, match="Mirror"):
+        fresh.upload_desc(d)
+    fresh.close()

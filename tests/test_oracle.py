@@ -1,0 +1,136 @@
+"""The oracle (CPU restatement) against known answers and its committed golden
+fixtures. Known answers are hand-derived from the reference formulas
+(geom.rs:56-93 sphere, geom.rs:504-533 Möller-Trumbore, world.rs:65-79 trace),
+so they hold for the reference itself; furnace scenes give exact radiance
+independent of the RNG."""
+import numpy as np
+import pytest
+
+import massrt
+import oracle
+
+ASPECT = float(massrt.ASPECT_RATIO)
+INF = float("inf")
+
+
+def lambert_world(o, color=(1, 1, 1, 1)):
+    s = o.solid(*color)
+    return o.material(1, s)
+
+
+def test_sphere_known_answers():
+    o = oracle.Scene(1)
+    m = lambert_world(o)
+    o.add_sphere(m, (0, 0, -5), 1.0)
+    o.build_bvh()
+    rays = np.array([[0, 0, 0, 0, 0, -1], [0, 0, -5, 0, 0, -1], [0, 0, 0, 0, 0, 1], [0, 3, 0, 0, 0, -1]],
+                    dtype=np.float32)
+    h = o.trace_rays(rays, 0.001, INF)
+    t = h[:, 2].view(np.float32)
+    assert h[0, 0] == (massrt.REF_SPHERE << 28) and t[0] == 4.0 and h[0, 3] == 1  # outside: near root, front
+    assert h[1, 0] == (massrt.REF_SPHERE << 28) and t[1] == 1.0 and h[1, 3] == 0  # inside: far root, back face
+    assert h[2, 0] == 0 and h[3, 0] == 0  # misses
+    # t_max is inclusive (geom.rs:70): a hit exactly at t_max is accepted
+    assert o.trace_rays(rays[:1], 0.001, 4.0)[0, 0] != 0
+    assert o.trace_rays(rays[:1], 0.001, np.nextafter(np.float32(4.0), np.float32(0)))[0, 0] == 0
+
+
+def test_triangle_known_answer():
+    o = oracle.Scene(1)
+    m = lambert_world(o)
+    o.add_triangle(m, [0, 0, -2, 1, 0, -2, 0, 1, -2])
+    o.build_bvh()
+    rays = np.array([[0.25, 0.25, 0, 0, 0, -1], [0.75, 0.75, 0, 0, 0, -1], [0.25, 0.25, 0, 1, 0, 0]],
+                    dtype=np.float32)
+    h = o.trace_rays(rays)
+    assert h[0, 0] == (massrt.REF_TRIANGLE << 28) and h[0, 2].view(np.float32) == 2.0
+    assert h[1, 0] == 0  # u + v > 1
+    assert h[2, 0] == 0  # |det| < 1e-6 (parallel)
+
+
+def test_ties_go_to_the_later_object():
+    # two identical spheres: BvhNode n=2 keeps the first left; the right child
+    # re-tests with t_max = left.t inclusive and wins (geom.rs:192-196)
+    for build in (True, False):
+        o = oracle.Scene(1)
+        m = lambert_world(o)
+        o.add_sphere(m, (0, 0, -5), 1.0)
+        o.add_sphere(m, (0, 0, -5), 1.0)
+        if build:
+            o.build_bvh()
+        h = o.trace_rays(np.array([[0, 0, 0, 0, 0, -1]], dtype=np.float32))
+        assert h[0, 0] == (massrt.REF_SPHERE << 28) | 1
+
+
+def furnace(kind, param=0.0):
+    o = oracle.Scene(1)
+    o.background(0, 0, (1.0, 1.0, 1.0))
+    s = o.solid(1, 1, 1, 1)
+    m = o.material(kind, s, param)
+    o.add_sphere(m, (0, 0, 0), 1.0)
+    o.build_bvh()
+    o.camera(40.0, (0, 0, 4), (0, 0, 0), aspect=ASPECT)
+    return o
+
+
+@pytest.mark.parametrize("kind,param", [(1, 0.0), (2, 0.0), (3, 1.5)])
+def test_furnace_exact(kind, param):
+    """White materials under a white sky: every sample's radiance is a product
+    of 1.0s, i.e. exactly 1 (or 0 for depth-exhausted / absorbed paths)."""
+    o = furnace(kind, param)
+    spp = 8
+    rgb, b = o.render(24, 16, 0, spp, seed=5, threads=4)
+    rgb = rgb.reshape(-1, 3)
+    assert np.all(rgb == np.round(rgb)) and rgb.max() == spp
+    assert np.all(rgb[:, 0] == rgb[:, 1]) and np.all(rgb[:, 1] == rgb[:, 2])
+    if kind == 1:
+        assert np.all(rgb == spp) and b.max() <= spp  # convex Lambertian: one bounce, never absorbed
+
+
+def test_golden_fixtures_reproduce(golden_dir):
+    g = np.load(golden_dir / "oracle_golden.npz")
+    for s in ["cornell", "sphere_grid", "cube_field"]:
+        o = oracle.Scene(1).builtin(s, ASPECT, golden_dir)
+        rgb, b = o.render(32, 18, 0, 2, seed=3, threads=3)
+        assert np.array_equal(b, g[f"{s}_bounces"]), s
+        assert np.array_equal(rgb.view(np.uint32), g[f"{s}_rgb"].view(np.uint32)), s
+        assert np.array_equal(o.trace_rays(g["rays"]), g[f"{s}_hits"]), s
+
+
+def test_render_is_deterministic_and_additive(golden_dir):
+    """Threads do not change results; [0,4) == [0,2)+[2,4) bit for bit (merge in sample order)."""
+    o = oracle.Scene(1).builtin("cornell", ASPECT, golden_dir)
+    a = o.render(20, 12, 0, 4, seed=9, threads=1)
+    b = o.render(20, 12, 0, 4, seed=9, threads=7)
+    c = o.render(20, 12, 0, 2, seed=9, threads=2)
+    c = o.render(20, 12, 2, 2, seed=9, threads=5, accum=c)
+    for x in (b, c):
+        assert np.array_equal(a[0].view(np.uint32), x[0].view(np.uint32)) and np.array_equal(a[1], x[1])
+
+
+def test_shards_partition_the_frame(golden_dir):
+    o = oracle.Scene(1).builtin("sphere_grid", ASPECT, golden_dir)
+    full = o.render(40, 24, 0, 1, seed=2, threads=4)
+    parts = [o.render(40, 24, 0, 1, seed=2, shard_index=i, shard_count=3, threads=2) for i in range(3)]
+    covered = sum((p[1] > 0) | (p[0].reshape(-1, 3).sum(1) > 0) for p in parts)
+    assert covered.max() <= 1
+    rgb = sum(p[0] for p in parts)
+    assert np.array_equal(rgb.view(np.uint32), full[0].view(np.uint32))
+    assert np.array_equal(sum(p[1] for p in parts), full[1])
+
+
+def test_render_pixels_matches_render(golden_dir):
+    o = oracle.Scene(1).builtin("cube_field", ASPECT, golden_dir)
+    W, H = 30, 17
+    rgb, b = o.render(W, H, 0, 3, seed=4, threads=4)
+    px = np.array([0, 5, 77, 299, W * H - 1], dtype=np.uint32)
+    prgb, pb = o.render_pixels(W, H, px, 0, 3, seed=4, threads=2)
+    assert np.array_equal(prgb.reshape(-1, 3), rgb.reshape(-1, 3)[px]) and np.array_equal(pb, b[px])
+
+
+def test_depth_limits(golden_dir):
+    o = oracle.Scene(1).builtin("sphere_grid", ASPECT, golden_dir)
+    rgb, b = o.render(16, 9, 0, 2, seed=1, max_depth=0, threads=2)
+    assert not rgb.any() and not b.any()  # trace(ray, 0) = (0, 0) (world.rs:66-67)
+    rgb, b = o.render(16, 9, 0, 2, seed=1, max_depth=1, threads=2)
+    assert b.max() <= 2
