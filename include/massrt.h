@@ -238,6 +238,9 @@ int mrt_trace_rays(mrt_ctx* ctx, const float* rays, uint32_t n, float t_min, flo
 int mrt_get_counters(mrt_ctx* ctx, mrt_counters* out);
 int mrt_reset_counters(mrt_ctx* ctx);
 int mrt_get_kernel_stats(mrt_ctx* ctx, mrt_kernel_stats* out);
+/* Self-test of the device's correctly rounded division (box slab test):
+ * n random/structured operand pairs vs IEEE a/b; mismatches must be 0. */
+int mrt_selftest_division(mrt_ctx* ctx, uint64_t n, uint64_t seed, uint64_t* mismatches);
 int mrt_reset_kernel_stats(mrt_ctx* ctx);
 /* bytes of device memory held for the scene */
 int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);

@@ -62,6 +62,7 @@ struct DevScene {
   const GpuMaterial* materials;
   const GpuTexture* textures;
   const uint32_t* texels;  // RGBA8 packed little-endian
+  uint32_t fast_ok;  // every box coordinate in {0} U [2^-40, 2^28] (path.h div fast path)
   uint32_t bg_kind;
   uint32_t bg_texture;  // SkySphere texture (surface must be a texture or solid)
   uint32_t bg_surf_kind;

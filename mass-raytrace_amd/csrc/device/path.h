@@ -83,11 +83,99 @@ MRT_DEV V4 surface_get_f(const DevScene& S, const GpuMaterial& m, V2 uv, LocalCo
 }
 
 // ---- primitive tests -------------------------------------------------------
-// BoundingBox::hit: 6 true divisions; the per-axis early-outs cannot change the
-// result (t0 only grows, t1 only shrinks), so one final compare is equivalent.
-MRT_DEV bool box_hit(V3 mn, V3 mx, V3 o, V3 d, float tmin, float tmax) {
-  V3 a = (mn - o) / d;
-  V3 b = (mx - o) / d;
+// Correctly rounded quotient a/b from y = RN(1/b) (computed once per ray with
+// a true IEEE division): q0 = a*y can be ~2 ulp off; one FMA residual
+// correction makes it faithful and a second rounds it exactly (Markstein's
+// theorem: y within 1/2 ulp of 1/b + faithful q => RN(q + (a - bq)y) = RN(a/b),
+// absent under/overflow). Results outside [2^-90, 2^90], dividends below
+// 2^-100 and divisors outside [2^-60, 2^60] take the plain division. 1 mul + 4 fma instead of the ~10
+// instruction v_div_scale/v_rcp/v_div_fmas/v_div_fixup sequence; verified
+// bit-exact against `a / b` by mrt_selftest_division.
+struct Recip {
+  float b, y;
+  bool ok;
+};
+MRT_DEV Recip make_recip(float b) {
+  Recip r;
+  r.b = b;
+  r.y = 1.0f / b;
+  r.ok = fabsf(b) >= 0x1p-60f && fabsf(b) <= 0x1p60f;
+  return r;
+}
+// q ~ RN(a/b): exact whenever div_in_range(q, a) and the divisor was `ok`
+MRT_DEV float div_fast(float a, const Recip& r) {
+  float q = a * r.y;
+  float e = fmaf(-q, r.b, a);
+  q = fmaf(e, r.y, q);
+  e = fmaf(-q, r.b, a);
+  return fmaf(e, r.y, q);
+}
+// fast path valid: quotient in [2^-90, 2^90] and dividend >= 2^-100 (else the
+// FMA residual a - q*b can fall into the subnormal range and lose bits)
+MRT_DEV bool div_in_range(float q, float a) {
+  float aq = fabsf(q);
+  return (aq <= 0x1p90f && aq >= 0x1p-90f && fabsf(a) >= 0x1p-100f) || a == 0.0f;
+}
+MRT_DEV float div_cr(float a, const Recip& r) {
+  float q = div_fast(a, r);
+  if (!r.ok || !div_in_range(q, a)) q = a / r.b;
+  return q;
+}
+// Ray in the space being traversed (world, or an instance's object space)
+// with what the slab test needs: y = RN(1/d) per axis and 1/|d|^2.
+struct TRay {
+  V3 o, d;
+  float yx, yy, yz;
+  Recip a;    // |d|^2 for Sphere::intersect
+  bool fast;  // every slab quotient of this ray can take div_fast exactly
+};
+// Fast-path domain: with every box coordinate and ray-origin coordinate in
+// {0} U [2^-40, 2^28] (scene bound checked on the host, origin here) each
+// nonzero numerator (min - o) is >= 2^-63 and < 2^29; with |d| in
+// [2^-20, 2^20] every quotient lies in [2^-83, 2^49] — inside div_fast's
+// exact range — so no per-quotient check is needed.
+MRT_DEV bool coord_ok(float c) {
+  float a = fabsf(c);
+  return a == 0.0f || (a >= 0x1p-40f && a <= 0x1p28f);
+}
+MRT_DEV bool dir_ok(float c) {
+  float a = fabsf(c);
+  return a >= 0x1p-20f && a <= 0x1p20f;
+}
+MRT_DEV TRay make_tray(V3 o, V3 d, bool scene_fast) {
+  TRay r;
+  r.o = o;
+  r.d = d;
+  r.yx = 1.0f / d.x;
+  r.yy = 1.0f / d.y;
+  r.yz = 1.0f / d.z;
+  r.a = make_recip(length_squared(d));
+  r.fast = scene_fast && coord_ok(o.x) && coord_ok(o.y) && coord_ok(o.z) && dir_ok(d.x) && dir_ok(d.y) &&
+           dir_ok(d.z);
+  return r;
+}
+MRT_DEV float qfast(float a, float b, float y) {
+  float q = a * y;
+  float e = fmaf(-q, b, a);
+  q = fmaf(e, y, q);
+  e = fmaf(-q, b, a);
+  return fmaf(e, y, q);
+}
+
+// BoundingBox::hit: v_min = (min - o)/d, v_max = (max - o)/d (6 correctly
+// rounded divisions); the per-axis early-outs cannot change the result (t0
+// only grows, t1 only shrinks), so one final compare is equivalent.
+template <bool FAST>
+MRT_DEV bool box_hit(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) {
+  V3 na = mn - r.o, nb = mx - r.o;
+  V3 a, b;
+  if (FAST) {
+    a = V3{qfast(na.x, r.d.x, r.yx), qfast(na.y, r.d.y, r.yy), qfast(na.z, r.d.z, r.yz)};
+    b = V3{qfast(nb.x, r.d.x, r.yx), qfast(nb.y, r.d.y, r.yy), qfast(nb.z, r.d.z, r.yz)};
+  } else {
+    a = na / r.d;
+    b = nb / r.d;
+  }
   V3 lo = vmin(a, b), hi = vmax(a, b);
   float t0 = fmaxf(lo.x, tmin), t1 = fminf(hi.x, tmax);
   t0 = fmaxf(lo.y, t0), t1 = fminf(hi.y, t1);
@@ -95,17 +183,17 @@ MRT_DEV bool box_hit(V3 mn, V3 mx, V3 o, V3 d, float tmin, float tmax) {
   return !(t1 < t0);
 }
 
-MRT_DEV bool sphere_hit(V3 c, float r, V3 o, V3 d, float tmin, float tmax, float& t) {
+MRT_DEV bool sphere_hit(V3 c, float r, V3 o, V3 d, const Recip& ra, float tmin, float tmax, float& t) {
   V3 oc = o - c;
-  float a = length_squared(d);
+  float a = ra.b;  // length_squared(d), precomputed per ray
   float half_b = dot(oc, d);
   float cc = length_squared(oc) - (r * r);
   float disc = (half_b * half_b) - (a * cc);
   if (disc < 0.0f) return false;
   float sq = sqrtf(disc);
-  float root = (-half_b - sq) / a;
+  float root = div_cr(-half_b - sq, ra);
   if (root < tmin || tmax < root) {
-    root = (-half_b + sq) / a;
+    root = div_cr(-half_b + sq, ra);
     if (root < tmin || tmax < root) return false;
   }
   t = root;
@@ -192,25 +280,27 @@ struct Hit {
 };
 
 // World::intersect(ray, t_min, t_max) over the preorder stream.
-template <bool COUNT>
-MRT_DEV Hit closest_hit(const DevScene& S, V3 o, V3 d, float tmin, float tmax, LocalCounters& lc) {
+// World::intersect over the preorder stream. FAST=true uses div_fast in the
+// slab test and gives up (returns false) when an instance's object-space ray
+// leaves the fast domain; the caller then re-runs with FAST=false, which
+// gives the same answer — only the arithmetic path differs, not the result.
+template <bool FAST, bool COUNT>
+MRT_DEV bool traverse(const DevScene& S, const TRay& world, float tmin, float tmax, Hit& h, LocalCounters& lc) {
   const uint4* slots = reinterpret_cast<const uint4*>(S.slots);
-  uint32_t i = S.world_begin, end = S.world_end, ret = 0;
-  bool in_blas = false;
-  V3 ro = o, rd = d;
+  uint32_t i = S.world_begin, end = S.world_end, ret = 0xFFFFFFFFu;
+  TRay r = world;
   uint32_t container = kRefNone;
-  Hit h{tmax, kRefNone, kRefNone};
+  h = Hit{tmax, kRefNone, kRefNone};
   float best = tmax;
   for (;;) {
     if (i >= end) {
-      if (!in_blas) break;
-      in_blas = false;
-      i = ret;
+      if (ret == 0xFFFFFFFFu) break;
+      i = ret;  // leave the BLAS: back to the world ray (geom.rs:405-409)
       end = S.world_end;
-      ro = o;
-      rd = d;
+      ret = 0xFFFFFFFFu;
+      r = world;
       container = kRefNone;
-      continue;
+      if (i >= end) break;
     }
     const uint4 s0 = slots[i];
     const uint4 s1 = slots[i + 1];
@@ -218,15 +308,17 @@ MRT_DEV Hit closest_hit(const DevScene& S, V3 o, V3 d, float tmin, float tmax, L
     if (kind == KIND_BOX) {
       if (COUNT) lc.node_visits++;
       V3 mn{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, mx{u2f(s0.w), u2f(s1.x), u2f(s1.y)};
-      i = box_hit(mn, mx, ro, rd, tmin, best) ? i + 2 : s1.z;
-    } else if (kind == KIND_TRI) {
+      i = box_hit<FAST>(mn, mx, r, tmin, best) ? i + 2 : s1.z;
+      continue;
+    }
+    if (kind == KIND_TRI) {
       if (COUNT) lc.triangle_tests++;
       const uint4 s2 = slots[i + 2];
       V3 a{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, ab{u2f(s0.w), u2f(s1.x), u2f(s1.y)},
           ac{u2f(s2.x), u2f(s2.y), u2f(s2.z)};
       float t;
-      if (tri_hit(a, ab, ac, ro, rd, tmin, best, t)) {
-        if (!(s2.w & TRI_FLAG_ALPHA) || tri_alpha_pass(S, s1.z, ro, rd, t, lc)) {
+      if (tri_hit(a, ab, ac, r.o, r.d, tmin, best, t)) {
+        if (!(s2.w & TRI_FLAG_ALPHA) || tri_alpha_pass(S, s1.z, r.o, r.d, t, lc)) {
           best = t;
           h.t = t;
           h.prim = make_ref(MRT_REF_TRIANGLE, s1.z);
@@ -237,7 +329,7 @@ MRT_DEV Hit closest_hit(const DevScene& S, V3 o, V3 d, float tmin, float tmax, L
     } else if (kind == KIND_SPHERE) {
       if (COUNT) lc.sphere_tests++;
       float t;
-      if (sphere_hit(V3{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, u2f(s0.w), ro, rd, tmin, best, t)) {
+      if (sphere_hit(V3{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, u2f(s0.w), r.o, r.d, r.a, tmin, best, t)) {
         best = t;
         h.t = t;
         h.prim = make_ref(MRT_REF_SPHERE, s1.x);
@@ -248,22 +340,35 @@ MRT_DEV Hit closest_hit(const DevScene& S, V3 o, V3 d, float tmin, float tmax, L
       if (COUNT) lc.instance_entries++;
       V3 c0, c1, c2, c3;
       load_m12(S.inst_inv + (size_t)s0.x * 12, c0, c1, c2, c3);
-      ro = xform(c0, c1, c2, c3, o, 1.0f);
-      rd = xform(c0, c1, c2, c3, d, 0.0f);
+      r = make_tray(xform(c0, c1, c2, c3, world.o, 1.0f), xform(c0, c1, c2, c3, world.d, 0.0f), S.fast_ok);
+      if (FAST && !r.fast) return false;
       container = make_ref(MRT_REF_INSTANCE, s0.x);
       ret = i + 2;
       i = s0.y;
       end = s0.z;
-      in_blas = true;
     } else {  // KIND_MODEL
       if (COUNT) lc.model_entries++;
       container = make_ref(MRT_REF_MODEL, s0.x);
       ret = i + 2;
       i = s0.y;
       end = s0.z;
-      in_blas = true;
     }
   }
+  return true;
+}
+
+template <bool COUNT>
+MRT_DEV Hit closest_hit(const DevScene& S, V3 o, V3 d, float tmin, float tmax, LocalCounters& lc) {
+  const TRay world = make_tray(o, d, S.fast_ok);
+  Hit h;
+  if (world.fast) {
+    LocalCounters trial = lc;
+    if (traverse<true, COUNT>(S, world, tmin, tmax, h, trial)) {
+      lc = trial;
+      return h;
+    }
+  }
+  traverse<false, COUNT>(S, world, tmin, tmax, h, lc);
   return h;
 }
 

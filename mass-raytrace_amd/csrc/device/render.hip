@@ -268,6 +268,70 @@ __global__ __launch_bounds__(kBlock) void k_trace_rays(DevScene S, const float* 
   flush_counters(cnt, lc, seg, nh, 0, 0);
 }
 
+// div_cr (path.h) against the IEEE division on random bit patterns plus
+// structured operands (all-ones / power-of-two mantissas, range edges).
+__global__ __launch_bounds__(kBlock) void k_selftest_division(unsigned long long n, unsigned long long seed,
+                                                              unsigned long long* mismatches) {
+  unsigned long long bad = 0;
+  const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
+  for (unsigned long long i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    uint64_t x = seed ^ (i * 0x9E3779B97F4A7C15ull);
+    unsigned long long r1 = splitmix64_next(x), r2 = splitmix64_next(x);
+    uint32_t ua = (uint32_t)r1, ub = (uint32_t)(r1 >> 32);
+    switch (r2 & 7) {
+      case 0:  // all-ones divisor mantissa
+        ub |= 0x007FFFFFu;
+        break;
+      case 1:  // power-of-two divisor
+        ub &= 0xFF800000u;
+        break;
+      case 2:  // all-ones dividend mantissa
+        ua |= 0x007FFFFFu;
+        break;
+      case 3:  // scene-like magnitudes: exponents near 1
+        ua = (ua & 0x807FFFFFu) | ((120u + ((uint32_t)(r2 >> 8) % 20u)) << 23);
+        ub = (ub & 0x807FFFFFu) | ((110u + ((uint32_t)(r2 >> 16) % 30u)) << 23);
+        break;
+      case 4:  // quotient near 1 ulp ties: a = b * small integer
+        ub = (ub & 0x807FFFFFu) | (127u << 23);
+        {
+          float fa = __uint_as_float(ub) * (float)((r2 >> 8) & 0xFFFF);
+          ua = __float_as_uint(fa) ^ (uint32_t)((r2 >> 32) & 3);
+        }
+        break;
+      default:
+        break;
+    }
+    float a = __uint_as_float(ua), b = __uint_as_float(ub);
+    float q;
+    if ((r2 & 7) >= 5) {
+      // the slab test's fast domain (path.h TRay::fast): a = m - o with m, o in
+      // {0} U [2^-40, 2^28], |b| in [2^-20, 2^20]; q = qfast(a, b, RN(1/b))
+      auto coord = [](uint32_t bits, uint32_t sel) {
+        uint32_t e = 87u + (sel % 68u);  // 2^-40 .. 2^27
+        float v = __uint_as_float((bits & 0x807FFFFFu) | (e << 23));
+        return (sel & 15u) == 0 ? 0.0f : v;
+      };
+      float m = coord(ua, (uint32_t)(r2 >> 8)), o = coord(ub, (uint32_t)(r2 >> 24));
+      if ((r2 >> 40) & 1) o = m;  // zero numerators
+      if (((r2 >> 42) & 3) == 0 && m != 0.0f)  // cancellation: o a few ulps from m
+        o = __uint_as_float(__float_as_uint(m) + (uint32_t)((r2 >> 44) & 7));
+      a = m - o;
+      uint32_t eb = 107u + ((uint32_t)(r2 >> 48) % 40u);  // 2^-20 .. 2^19
+      b = __uint_as_float((ub & 0x807FFFFFu) | (eb << 23));
+      q = qfast(a, b, 1.0f / b);
+    } else {
+      q = div_cr(a, make_recip(b));
+    }
+    float ref = a / b;
+    uint32_t uq = __float_as_uint(q), ur = __float_as_uint(ref);
+    bool same = uq == ur || (q != q && ref != ref) || (q == 0.0f && ref == 0.0f);
+    bad += same ? 0 : 1;
+  }
+  bad = (unsigned long long)wave_sum((uint32_t)bad);
+  if (lane_id() == 0 && bad) atomicAdd(mismatches, bad);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -640,6 +704,7 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     S.materials = (const GpuMaterial*)(base + o_mat);
     S.textures = (const GpuTexture*)(base + o_tex);
     S.texels = (const uint32_t*)(base + o_texel);
+    S.fast_ok = hs.fast_ok;
     S.bg_kind = hs.bg_kind;
     S.bg_texture = hs.bg_texture;
     S.bg_surf_kind = hs.bg_surf_kind;
@@ -761,6 +826,23 @@ int mrt_get_kernel_stats(mrt_ctx* c, mrt_kernel_stats* out) {
 
 int mrt_reset_kernel_stats(mrt_ctx* c) {
   return guarded(c, [&] { c->kstats = mrt_kernel_stats{}; });
+}
+
+int mrt_selftest_division(mrt_ctx* c, uint64_t n, uint64_t seed, uint64_t* mismatches) {
+  return guarded(c, [&] {
+    if (!mismatches) throw ApiError{MRT_ERR_INVALID, "null output"};
+    unsigned long long* d = nullptr;
+    HIP_CHECK(hipMalloc(&d, 8));
+    HIP_CHECK(hipMemsetAsync(d, 0, 8, c->stream));
+    hipLaunchKernelGGL(k_selftest_division, dim3(4096), dim3(kBlock), 0, c->stream, (unsigned long long)n,
+                       (unsigned long long)seed, d);
+    HIP_CHECK(hipGetLastError());
+    unsigned long long h = 0;
+    HIP_CHECK(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    HIP_CHECK(hipFree(d));
+    *mismatches = h;
+  });
 }
 
 int mrt_reset_counters(mrt_ctx* c) {

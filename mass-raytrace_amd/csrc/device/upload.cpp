@@ -1,6 +1,7 @@
 // upload.cpp — linearise the reference BVH into the preorder slot stream.
 #include "upload.h"
 
+#include <math.h>
 #include <string.h>
 
 #include <unordered_map>
@@ -131,6 +132,13 @@ struct Emitter {
       if (idx >= d.n_nodes) return fail("node index out of range");
       if (++depth_guard > 4 * d.n_nodes + 16) return fail("BVH is not a tree (cycle)");
       const mrt_node& n = d.nodes[idx];
+      for (int k = 0; k < 3; ++k) {
+        float c[2] = {n.min[k], n.max[k]};
+        for (float v : c) {
+          float a = fabsf(v);
+          if (!(a == 0.0f || (a >= 0x1p-40f && a <= 0x1p28f))) s.fast_ok = 0;
+        }
+      }
       uint32_t at = push_slot(fbits(n.min[0]), fbits(n.min[1]), fbits(n.min[2]), fbits(n.max[0]));
       push_slot(fbits(n.max[1]), fbits(n.max[2]), 0, KIND_BOX);
       s.n_box_records++;

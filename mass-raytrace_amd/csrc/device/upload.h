@@ -19,6 +19,7 @@ struct HostScene {
   std::vector<GpuMaterial> materials;
   std::vector<GpuTexture> textures;
   std::vector<uint32_t> texels;
+  uint32_t fast_ok = 1;
   uint32_t bg_kind = 0, bg_texture = 0, bg_surf_kind = 0;
   float bg_color[4] = {0, 0, 0, 0};
   // statistics

@@ -145,7 +145,7 @@ EXPORTED_SYMBOLS = [
     "mrt_create", "mrt_destroy", "mrt_last_error", "mrt_global_last_error", "mrt_abi_version",
     "mrt_upload_scene", "mrt_set_camera", "mrt_render", "mrt_render_device", "mrt_trace_rays",
     "mrt_get_counters", "mrt_reset_counters", "mrt_scene_device_bytes", "mrt_get_kernel_stats",
-    "mrt_reset_kernel_stats",
+    "mrt_reset_kernel_stats", "mrt_selftest_division",
     "mrt_builder_new", "mrt_builder_free", "mrt_builder_builtin", "mrt_builder_rand_f32", "mrt_builder_solid",
     "mrt_builder_texture_png", "mrt_builder_texture_rgba", "mrt_builder_material", "mrt_builder_background",
     "mrt_builder_add_sphere", "mrt_builder_add_triangle", "mrt_builder_model", "mrt_builder_model_from_ply",
@@ -182,6 +182,7 @@ def lib() -> C.CDLL:
         "mrt_reset_counters": (I, [P]),
         "mrt_get_kernel_stats": (I, [P, C.POINTER(MrtKernelStats)]),
         "mrt_reset_kernel_stats": (I, [P]),
+        "mrt_selftest_division": (I, [P, U64, U64, C.POINTER(C.c_uint64)]),
         "mrt_scene_device_bytes": (I, [P, C.POINTER(C.c_uint64)]),
         "mrt_builder_new": (I, [U64, C.POINTER(P)]),
         "mrt_builder_free": (I, [P]),
@@ -437,6 +438,11 @@ class Context:
         k = MrtKernelStats()
         self._check(lib().mrt_get_kernel_stats(self.h, C.byref(k)))
         return k.as_dict()
+
+    def selftest_division(self, n: int, seed: int = 1) -> int:
+        m = C.c_uint64()
+        self._check(lib().mrt_selftest_division(self.h, n, seed, C.byref(m)))
+        return int(m.value)
 
     def reset_kernel_stats(self):
         self._check(lib().mrt_reset_kernel_stats(self.h))

@@ -251,3 +251,10 @@ def test_errors_are_reported(ctx):
     with pytest.raises(massrt.MassrtError, match="Mirror"):
         fresh.upload_desc(d)
     fresh.close()
+
+
+def test_device_division_is_correctly_rounded(ctx):
+    """The box/sphere tests replace IEEE division by a reciprocal + two FMA
+    corrections (path.h div_cr); it must equal a/b bit for bit."""
+    assert ctx.selftest_division(1 << 30, seed=1) == 0
+    assert ctx.selftest_division(1 << 28, seed=12345) == 0
