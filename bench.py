@@ -178,8 +178,7 @@ def main():
         seg_per_sample = cnt["segments"] / cnt["samples"]
         bytes_per_seg = (sum(TRACE_BYTES[k] * cnt[k] for k in TRACE_BYTES) / max(cnt["segments"], 1)
                          + TRACE_RAY_BYTES)
-        my_samples = cnt["samples"] / max(cnt["samples"], 1) * (samples_total / world)
-        segs = seg_per_sample * my_samples
+        segs = seg_per_sample * (samples_total / world)  # this rank's share of the timed samples
         achieved = bytes_per_seg * segs / (ks["trace_ms"] * 1e-3) / 1e9
         traffic = None
         pmc = Path(a.pmc_json) if a.pmc_json else REPO / "profiles" / f"pmc_{a.scene}.json"

@@ -187,6 +187,7 @@ typedef struct {
 } mrt_render_args;
 #define MRT_RENDER_COUNTERS 1u     /* collect traversal counters (slower) */
 #define MRT_RENDER_TIME_KERNELS 2u /* time every k_trace/k_shade launch with HIP events */
+#define MRT_RENDER_SIMPLE_TRACE 4u /* debug: one-ray-per-thread closest hit instead of the persistent k_trace */
 
 /* Closest hit of one ray (parity entry point). */
 typedef struct {
@@ -241,6 +242,12 @@ int mrt_get_kernel_stats(mrt_ctx* ctx, mrt_kernel_stats* out);
 /* Self-test of the device's correctly rounded division (box slab test):
  * n random/structured operand pairs vs IEEE a/b; mismatches must be 0. */
 int mrt_selftest_division(mrt_ctx* ctx, uint64_t n, uint64_t seed, uint64_t* mismatches);
+/* Debug builds (-DMRT_DEBUG_BOUNDS, libmassrt_dbg.so) check every scene and
+ * path-buffer index on the device and record the first failure here as
+ * {check code, index, bound, failure count} instead of faulting.
+ * mrt_debug_build() reports whether the loaded library is such a build. */
+int mrt_debug_status(mrt_ctx* ctx, uint32_t* out4);
+int mrt_debug_build(void);
 int mrt_reset_kernel_stats(mrt_ctx* ctx);
 /* bytes of device memory held for the scene */
 int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);

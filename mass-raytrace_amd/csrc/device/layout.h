@@ -63,6 +63,9 @@ struct DevScene {
   const GpuTexture* textures;
   const uint32_t* texels;  // RGBA8 packed little-endian
   uint32_t fast_ok;  // every box coordinate in {0} U [2^-40, 2^28] (path.h div fast path)
+  // array sizes (checked only in MRT_DEBUG_BOUNDS builds) and the debug record
+  uint32_t n_slots, n_tris, n_sph, n_inst, n_models, n_materials, n_textures, n_texels;
+  uint32_t* dbg;  // {first failing check code, index, bound, failures}
   uint32_t bg_kind;
   uint32_t bg_texture;  // SkySphere texture (surface must be a texture or solid)
   uint32_t bg_surf_kind;

@@ -35,6 +35,25 @@ struct LocalCounters {
            texel_taps = 0;
 };
 
+// Bounds checks of every scene-array index, compiled in with
+// -DMRT_DEBUG_BOUNDS (libmassrt_dbg.so): a failing index is recorded in
+// S.dbg and replaced by 0, so a bad index shows up as a record instead of a
+// GPU memory fault.
+#ifdef MRT_DEBUG_BOUNDS
+MRT_DEV uint32_t mrt_chk(uint32_t* dbg, uint32_t idx, uint32_t bound, uint32_t code) {
+  if (idx < bound) return idx;
+  if (atomicCAS(dbg, 0u, code) == 0u) {
+    dbg[1] = idx;
+    dbg[2] = bound;
+  }
+  atomicAdd(dbg + 3, 1u);
+  return 0;
+}
+#define MRT_IDX(S, idx, bound, code) mrt_chk((S).dbg, (idx), (bound), (code))
+#else
+#define MRT_IDX(S, idx, bound, code) (idx)
+#endif
+
 MRT_DEV float u2f(uint32_t u) { return __uint_as_float(u); }
 MRT_DEV V3 ld3(const float* p) { return V3{p[0], p[1], p[2]}; }
 
@@ -44,13 +63,13 @@ MRT_DEV float rust_fract(float x) { return x - truncf(x); }
 MRT_DEV uint32_t f2usize(float f) { return f > 0.0f ? (f < 4294967040.0f ? (uint32_t)f : 0xFFFFFFFFu) : 0u; }
 
 MRT_DEV V4 texel(const DevScene& S, const GpuTexture& t, uint32_t x, uint32_t y) {
-  uint32_t v = S.texels[t.offset + y * t.width + x];
+  uint32_t v = S.texels[MRT_IDX(S, t.offset + y * t.width + x, S.n_texels, 1)];
   return V4{(float)(v & 255u) / 255.0f, (float)((v >> 8) & 255u) / 255.0f, (float)((v >> 16) & 255u) / 255.0f,
             (float)(v >> 24) / 255.0f};
 }
 
 MRT_DEV V4 texture_get_f(const DevScene& S, uint32_t tex, V2 uv, LocalCounters& lc) {
-  const GpuTexture t = S.textures[tex];
+  const GpuTexture t = S.textures[MRT_IDX(S, tex, S.n_textures, 2)];
   float x = uv.x, y = uv.y;
   if (t.wrap == MRT_WRAP_REPEAT) {
     x = x < 0.0f ? 1.0f - rust_fract(fabsf(x)) : x;
@@ -162,27 +181,6 @@ MRT_DEV float qfast(float a, float b, float y) {
   return fmaf(e, y, q);
 }
 
-// BoundingBox::hit: v_min = (min - o)/d, v_max = (max - o)/d (6 correctly
-// rounded divisions); the per-axis early-outs cannot change the result (t0
-// only grows, t1 only shrinks), so one final compare is equivalent.
-template <bool FAST>
-MRT_DEV bool box_hit(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) {
-  V3 na = mn - r.o, nb = mx - r.o;
-  V3 a, b;
-  if (FAST) {
-    a = V3{qfast(na.x, r.d.x, r.yx), qfast(na.y, r.d.y, r.yy), qfast(na.z, r.d.z, r.yz)};
-    b = V3{qfast(nb.x, r.d.x, r.yx), qfast(nb.y, r.d.y, r.yy), qfast(nb.z, r.d.z, r.yz)};
-  } else {
-    a = na / r.d;
-    b = nb / r.d;
-  }
-  V3 lo = vmin(a, b), hi = vmax(a, b);
-  float t0 = fmaxf(lo.x, tmin), t1 = fminf(hi.x, tmax);
-  t0 = fmaxf(lo.y, t0), t1 = fminf(hi.y, t1);
-  t0 = fmaxf(lo.z, t0), t1 = fminf(hi.z, t1);
-  return !(t1 < t0);
-}
-
 MRT_DEV bool sphere_hit(V3 c, float r, V3 o, V3 d, const Recip& ra, float tmin, float tmax, float& t) {
   V3 oc = o - c;
   float a = ra.b;  // length_squared(d), precomputed per ray
@@ -223,7 +221,7 @@ struct TriShade {
   uint32_t material, flags;
 };
 MRT_DEV TriShade load_tri(const DevScene& S, uint32_t id) {
-  const float4* q = reinterpret_cast<const float4*>(S.tri_shade) + (size_t)id * kTriShadeQuads;
+  const float4* q = reinterpret_cast<const float4*>(S.tri_shade) + (size_t)MRT_IDX(S, id, S.n_tris, 3) * kTriShadeQuads;
   float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4], q5 = q[5], q6 = q[6];
   TriShade s;
   s.a = V3{q0.x, q0.y, q0.z};
@@ -257,7 +255,7 @@ MRT_DEV bool tri_alpha_pass(const DevScene& S, uint32_t id, V3 o, V3 d, float t,
   float a0, a1, a2;
   tri_bary(s, point, a0, a1, a2);
   V2 uv = (s.uva * a0 + s.uvb * a1) + s.uvc * a2;
-  const GpuMaterial m = S.materials[s.material];
+  const GpuMaterial m = S.materials[MRT_IDX(S, s.material, S.n_materials, 4)];
   if (m.kind != MRT_MAT_LAMBERTIAN && m.kind != MRT_MAT_METAL) return true;
   return surface_get_f(S, m, uv, lc).w != 0.0f;
 }
@@ -280,96 +278,177 @@ struct Hit {
 };
 
 // World::intersect(ray, t_min, t_max) over the preorder stream.
-// World::intersect over the preorder stream. FAST=true uses div_fast in the
-// slab test and gives up (returns false) when an instance's object-space ray
-// leaves the fast domain; the caller then re-runs with FAST=false, which
-// gives the same answer — only the arithmetic path differs, not the result.
-template <bool FAST, bool COUNT>
-MRT_DEV bool traverse(const DevScene& S, const TRay& world, float tmin, float tmax, Hit& h, LocalCounters& lc) {
-  const uint4* slots = reinterpret_cast<const uint4*>(S.slots);
-  uint32_t i = S.world_begin, end = S.world_end, ret = 0xFFFFFFFFu;
-  TRay r = world;
-  uint32_t container = kRefNone;
-  h = Hit{tmax, kRefNone, kRefNone};
-  float best = tmax;
-  for (;;) {
-    if (i >= end) {
-      if (ret == 0xFFFFFFFFu) break;
-      i = ret;  // leave the BLAS: back to the world ray (geom.rs:405-409)
-      end = S.world_end;
-      ret = 0xFFFFFFFFu;
-      r = world;
-      container = kRefNone;
-      if (i >= end) break;
+// World::intersect over the preorder stream, one record per step so that a
+// persistent kernel can interleave many rays per lane (render.hip k_trace).
+// Each lane's sequence of box/primitive tests is exactly the reference's
+// (left-first recursion with shrinking t_max, geom.rs:185-205); only which
+// lanes of a wave are busy at a time differs.
+struct Trav {
+  TRay world, r;  // world ray, ray of the space being traversed
+  uint32_t i, end, ret, container;
+  float tmin, best;
+  Hit h;
+  uint4 s0, s1;  // current record (prefetched when i moves)
+  bool done;
+#ifdef MRT_DEBUG_BOUNDS
+  uint32_t steps;
+#endif
+};
+
+// f32 min/max without the canonicalising v_max hipcc inserts before fminf:
+// every operand here is an arithmetic result (never a signalling NaN), for
+// which v_min/v_max/v_min3/v_max3 are IEEE minNum/maxNum = Rust f32::min/max.
+MRT_DEV float vmin1(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+MRT_DEV float vmax1(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+MRT_DEV float vmin3(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+MRT_DEV float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// BoundingBox::hit (geom.rs:218-247): v_min = (min - o)/d, v_max = (max - o)/d,
+// six correctly rounded quotients — qfast in the ray's fast domain (bit-identical
+// to IEEE division there), IEEE division otherwise. The per-axis early-outs
+// cannot change the result (t0 only grows, t1 only shrinks, NaNs are ignored
+// by min/max): one final compare of max(tmin, lo) against min(tmax, hi).
+MRT_DEV bool box_hit_any(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) {
+  V3 na = mn - r.o, nb = mx - r.o;
+  V3 a{qfast(na.x, r.d.x, r.yx), qfast(na.y, r.d.y, r.yy), qfast(na.z, r.d.z, r.yz)};
+  V3 b{qfast(nb.x, r.d.x, r.yx), qfast(nb.y, r.d.y, r.yy), qfast(nb.z, r.d.z, r.yz)};
+  if (!r.fast) {
+    a = na / r.d;
+    b = nb / r.d;
+  }
+  float t0 = vmax3(vmin1(a.x, b.x), vmin1(a.y, b.y), vmax1(vmin1(a.z, b.z), tmin));
+  float t1 = vmin3(vmax1(a.x, b.x), vmax1(a.y, b.y), vmin1(vmax1(a.z, b.z), tmax));
+  return !(t1 < t0);
+}
+
+// Move to record t.i (leaving a finished BLAS region) and prefetch it.
+MRT_DEV void trav_fetch(const DevScene& S, Trav& t) {
+  if (t.i >= t.end) {
+    if (t.ret == 0xFFFFFFFFu) {
+      t.done = true;
+      return;
     }
-    const uint4 s0 = slots[i];
-    const uint4 s1 = slots[i + 1];
-    const uint32_t kind = s1.w;
-    if (kind == KIND_BOX) {
-      if (COUNT) lc.node_visits++;
-      V3 mn{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, mx{u2f(s0.w), u2f(s1.x), u2f(s1.y)};
-      i = box_hit<FAST>(mn, mx, r, tmin, best) ? i + 2 : s1.z;
-      continue;
-    }
-    if (kind == KIND_TRI) {
-      if (COUNT) lc.triangle_tests++;
-      const uint4 s2 = slots[i + 2];
-      V3 a{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, ab{u2f(s0.w), u2f(s1.x), u2f(s1.y)},
-          ac{u2f(s2.x), u2f(s2.y), u2f(s2.z)};
-      float t;
-      if (tri_hit(a, ab, ac, r.o, r.d, tmin, best, t)) {
-        if (!(s2.w & TRI_FLAG_ALPHA) || tri_alpha_pass(S, s1.z, r.o, r.d, t, lc)) {
-          best = t;
-          h.t = t;
-          h.prim = make_ref(MRT_REF_TRIANGLE, s1.z);
-          h.container = container;
-        }
-      }
-      i += 3;
-    } else if (kind == KIND_SPHERE) {
-      if (COUNT) lc.sphere_tests++;
-      float t;
-      if (sphere_hit(V3{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, u2f(s0.w), r.o, r.d, r.a, tmin, best, t)) {
-        best = t;
-        h.t = t;
-        h.prim = make_ref(MRT_REF_SPHERE, s1.x);
-        h.container = container;
-      }
-      i += 2;
-    } else if (kind == KIND_INST) {
-      if (COUNT) lc.instance_entries++;
-      V3 c0, c1, c2, c3;
-      load_m12(S.inst_inv + (size_t)s0.x * 12, c0, c1, c2, c3);
-      r = make_tray(xform(c0, c1, c2, c3, world.o, 1.0f), xform(c0, c1, c2, c3, world.d, 0.0f), S.fast_ok);
-      if (FAST && !r.fast) return false;
-      container = make_ref(MRT_REF_INSTANCE, s0.x);
-      ret = i + 2;
-      i = s0.y;
-      end = s0.z;
-    } else {  // KIND_MODEL
-      if (COUNT) lc.model_entries++;
-      container = make_ref(MRT_REF_MODEL, s0.x);
-      ret = i + 2;
-      i = s0.y;
-      end = s0.z;
+    t.i = t.ret;  // leave the BLAS: back to the world ray (geom.rs:405-409)
+    t.end = S.world_end;
+    t.ret = 0xFFFFFFFFu;
+    t.r = t.world;
+    t.container = kRefNone;
+    if (t.i >= t.end) {
+      t.done = true;
+      return;
     }
   }
-  return true;
+  const uint4* slots = reinterpret_cast<const uint4*>(S.slots);
+#ifdef MRT_DEBUG_BOUNDS
+  if (t.i + 1 >= S.n_slots || ++t.steps > (1u << 24)) {  // record and stop instead of looping/faulting
+    MRT_IDX(S, t.i + 1 >= S.n_slots ? t.i : 0xFFFFFFF0u, t.i + 1 >= S.n_slots ? S.n_slots : 0u, 5);
+    t.done = true;
+    return;
+  }
+#endif
+  t.s0 = slots[MRT_IDX(S, t.i, S.n_slots, 5)];
+  t.s1 = slots[MRT_IDX(S, t.i + 1, S.n_slots, 6)];
+}
+
+MRT_DEV void trav_init(const DevScene& S, Trav& t, V3 o, V3 d, float tmin, float tmax) {
+  t.world = make_tray(o, d, S.fast_ok);
+  t.r = t.world;
+  t.i = S.world_begin;
+  t.end = S.world_end;
+  t.ret = 0xFFFFFFFFu;
+  t.container = kRefNone;
+  t.tmin = tmin;
+  t.best = tmax;
+  t.h = Hit{tmax, kRefNone, kRefNone};
+  t.done = false;
+#ifdef MRT_DEBUG_BOUNDS
+  t.steps = 0;
+#endif
+  trav_fetch(S, t);
+}
+
+MRT_DEV bool trav_at_box(const Trav& t) { return t.s1.w == KIND_BOX; }
+
+// The current record is a box: test it and move on.
+template <bool COUNT>
+MRT_DEV void trav_box(const DevScene& S, Trav& t, LocalCounters& lc) {
+  if (COUNT) lc.node_visits++;
+  V3 mn{u2f(t.s0.x), u2f(t.s0.y), u2f(t.s0.z)}, mx{u2f(t.s0.w), u2f(t.s1.x), u2f(t.s1.y)};
+  t.i = box_hit_any(mn, mx, t.r, t.tmin, t.best) ? t.i + 2 : t.s1.z;
+  trav_fetch(S, t);
+}
+
+// The current record is a primitive, an instance or a model.
+template <bool COUNT>
+MRT_DEV void trav_prim(const DevScene& S, Trav& t, LocalCounters& lc) {
+  const uint4 s0 = t.s0, s1 = t.s1;
+  const uint32_t kind = s1.w;
+  if (kind == KIND_TRI) {
+    if (COUNT) lc.triangle_tests++;
+    const uint4 s2 = reinterpret_cast<const uint4*>(S.slots)[MRT_IDX(S, t.i + 2, S.n_slots, 7)];
+    V3 a{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, ab{u2f(s0.w), u2f(s1.x), u2f(s1.y)}, ac{u2f(s2.x), u2f(s2.y), u2f(s2.z)};
+    float th;
+    if (tri_hit(a, ab, ac, t.r.o, t.r.d, t.tmin, t.best, th)) {
+      if (!(s2.w & TRI_FLAG_ALPHA) || tri_alpha_pass(S, s1.z, t.r.o, t.r.d, th, lc)) {
+        t.best = th;
+        t.h = Hit{th, make_ref(MRT_REF_TRIANGLE, s1.z), t.container};
+      }
+    }
+    t.i += 3;
+  } else if (kind == KIND_SPHERE) {
+    if (COUNT) lc.sphere_tests++;
+    float th;
+    if (sphere_hit(V3{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, u2f(s0.w), t.r.o, t.r.d, t.r.a, t.tmin, t.best, th)) {
+      t.best = th;
+      t.h = Hit{th, make_ref(MRT_REF_SPHERE, s1.x), t.container};
+    }
+    t.i += 2;
+  } else if (kind == KIND_INST) {
+    if (COUNT) lc.instance_entries++;
+    V3 c0, c1, c2, c3;
+    load_m12(S.inst_inv + (size_t)MRT_IDX(S, s0.x, S.n_inst, 8) * 12, c0, c1, c2, c3);
+    t.r = make_tray(xform(c0, c1, c2, c3, t.world.o, 1.0f), xform(c0, c1, c2, c3, t.world.d, 0.0f), S.fast_ok);
+    t.container = make_ref(MRT_REF_INSTANCE, s0.x);
+    t.ret = t.i + 2;
+    t.i = s0.y;
+    t.end = s0.z;
+  } else {  // KIND_MODEL
+    if (COUNT) lc.model_entries++;
+    t.container = make_ref(MRT_REF_MODEL, s0.x);
+    t.ret = t.i + 2;
+    t.i = s0.y;
+    t.end = s0.z;
+  }
+  trav_fetch(S, t);
 }
 
 template <bool COUNT>
 MRT_DEV Hit closest_hit(const DevScene& S, V3 o, V3 d, float tmin, float tmax, LocalCounters& lc) {
-  const TRay world = make_tray(o, d, S.fast_ok);
-  Hit h;
-  if (world.fast) {
-    LocalCounters trial = lc;
-    if (traverse<true, COUNT>(S, world, tmin, tmax, h, trial)) {
-      lc = trial;
-      return h;
-    }
+  Trav t;
+  trav_init(S, t, o, d, tmin, tmax);
+  while (!t.done) {
+    if (trav_at_box(t))
+      trav_box<COUNT>(S, t, lc);
+    else
+      trav_prim<COUNT>(S, t, lc);
   }
-  traverse<false, COUNT>(S, world, tmin, tmax, h, lc);
-  return h;
+  return t.h;
 }
 
 // Hit record of the closest hit, computed the way the reference's winning
@@ -388,7 +467,7 @@ MRT_DEV Surf resolve_hit(const DevScene& S, V3 o, V3 d, const Hit& h) {
   V3 f0, f1, f2, f3;
   if (ckind == MRT_REF_INSTANCE) {
     V3 c0, c1, c2, c3;
-    load_m12(S.inst_inv + (size_t)cidx * 12, c0, c1, c2, c3);
+    load_m12(S.inst_inv + (size_t)MRT_IDX(S, cidx, S.n_inst, 9) * 12, c0, c1, c2, c3);
     ro = xform(c0, c1, c2, c3, o, 1.0f);
     rd = xform(c0, c1, c2, c3, d, 0.0f);
   }
@@ -396,12 +475,13 @@ MRT_DEV Surf resolve_hit(const DevScene& S, V3 o, V3 d, const Hit& h) {
   V3 outward;
   s.point = ro + rd * h.t;
   if (pkind == MRT_REF_SPHERE) {
-    V3 c = ld3(S.sph + (size_t)pidx * 4);
-    float r = S.sph[(size_t)pidx * 4 + 3];
+    const uint32_t sp = MRT_IDX(S, pidx, S.n_sph, 10);
+    V3 c = ld3(S.sph + (size_t)sp * 4);
+    float r = S.sph[(size_t)sp * 4 + 3];
     outward = (s.point - c) / r;
     s.has_uv = false;
     s.uv = V2{0, 0};
-    s.material = S.sph_mat[pidx];
+    s.material = S.sph_mat[sp];
   } else {
     TriShade t = load_tri(S, pidx);
     float a0, a1, a2;
@@ -415,13 +495,13 @@ MRT_DEV Surf resolve_hit(const DevScene& S, V3 o, V3 d, const Hit& h) {
   s.front_face = dot(rd, outward) < 0.0f;
   s.normal = s.front_face ? outward : -outward;
   if (ckind == MRT_REF_INSTANCE) {
-    load_m12(S.inst_fwd + (size_t)cidx * 12, f0, f1, f2, f3);
+    load_m12(S.inst_fwd + (size_t)MRT_IDX(S, cidx, S.n_inst, 11) * 12, f0, f1, f2, f3);
     s.point = xform(f0, f1, f2, f3, s.point, 1.0f);
     s.normal = unit(xform(f0, f1, f2, f3, s.normal, 0.0f));
-    uint32_t m = S.inst_mat[cidx];
+    uint32_t m = S.inst_mat[MRT_IDX(S, cidx, S.n_inst, 12)];
     if (m != MRT_NO_MATERIAL) s.material = m;
   } else if (ckind == MRT_REF_MODEL) {
-    uint32_t m = S.model_mat[cidx];
+    uint32_t m = S.model_mat[MRT_IDX(S, cidx, S.n_models, 13)];
     if (m != MRT_NO_MATERIAL) s.material = m;
   }
   return s;
@@ -492,7 +572,7 @@ MRT_DEV V3 background(const DevScene& S, V3 d, LocalCounters& lc) {
 // continues with (new_o, new_d) and attenuation `atten`.
 MRT_DEV bool scatter(const DevScene& S, const Surf& s, V3 d, PathRng& rng, V3& emitted, V3& atten, V3& new_d,
                      LocalCounters& lc) {
-  const GpuMaterial m = S.materials[s.material];
+  const GpuMaterial m = S.materials[MRT_IDX(S, s.material, S.n_materials, 4)];
   emitted = V3{0, 0, 0};
   V2 uv = s.has_uv ? s.uv : V2{0, 0};
   switch (m.kind) {

@@ -49,7 +49,7 @@ constexpr int kBlock = 256;
 struct Ctrl {
   uint32_t active[2];
   uint32_t next_work;
-  uint32_t pad;
+  uint32_t trace_next;  // persistent k_trace work counter (zeroed by k_shade)
 };
 
 // SoA path state, 5 x 16 B per slot:
@@ -71,6 +71,7 @@ struct RenderParams {
   uint32_t n_pix;        // pixels in this shard
   uint32_t G;            // work items in this chunk = n_pix * samples
   uint32_t sample_base;  // absolute sample index of chunk sample 0
+  uint32_t pool_cap;     // path slots per buffer
   const uint32_t* pixlist;
 };
 
@@ -99,7 +100,7 @@ __device__ __forceinline__ void gen_work(const DevCamera& cam, const RenderParam
                                          float4& rd, uint4& rs) {
   uint32_t s_local = g / rp.n_pix;
   uint32_t lp = g - s_local * rp.n_pix;
-  uint32_t p = rp.pixlist[lp];
+  uint32_t p = rp.pixlist[lp];  // lp < n_pix by construction (g < G)
   uint32_t y = p / rp.W, x = p - y * rp.W;
   PathRng rng = path_rng(rp.seed, p, rp.sample_base + s_local);
   V3 o, d;
@@ -122,24 +123,85 @@ __global__ __launch_bounds__(kBlock) void k_generate(DevCamera cam, RenderParams
   out.rng[i] = rs;
 }
 
+// Persistent closest-hit kernel: a fixed grid of waves pulls chunks of rays
+// from a counter; inside a wave a lane whose ray has finished takes the next
+// ray of the wave's chunk as soon as enough lanes are idle, so the SIMD keeps
+// issuing for busy lanes instead of waiting for the wave's slowest ray.
+constexpr float kTmin = 0.001f;          // World::intersect(ray, 0.001, INFINITY) (main.rs trace)
+constexpr uint32_t kTraceChunk = 256;  // rays per atomic grab
+constexpr uint32_t kRefill = 16;       // refill once this many lanes idle
+constexpr uint32_t kPrimBatch = 8;     // run the primitive branch once this many lanes wait at one
+
 template <bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
-                                                  DevCounters* cnt) {
+                                                  DevCounters* cnt, float tmin, float tmax) {
   const uint32_t n = ctrl->active[cur];
   if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = 0;
-  const uint32_t base = blockIdx.x * kBlock;
-  if (base >= n) return;
-  const uint32_t i = base + threadIdx.x;
+  if (n == 0) return;
   LocalCounters lc;
   uint32_t seg = 0, nh = 0;
-  if (i < n) {
-    float4 o4 = in.ro[i], d4 = in.rd[i];
-    Hit h = closest_hit<COUNT>(S, V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, 0.001f, INFINITY, lc);
-    hits[i] = make_uint4(__float_as_uint(h.t), h.prim, h.container, 0u);
-    seg = 1;
-    nh = h.prim != kRefNone;
+  uint32_t pool = 0, pool_end = 0;  // wave-uniform chunk [pool, pool_end)
+  bool drained = false;             // wave-uniform: the counter passed n
+  uint32_t ray = 0xFFFFFFFFu;
+  Trav t{};  // fully initialised: idle lanes must not carry undefined state
+  t.done = true;
+  for (;;) {
+    const unsigned long long idle = __ballot(ray == 0xFFFFFFFFu);
+    const uint32_t n_idle = (uint32_t)__popcll(idle);
+    if (n_idle >= kRefill || n_idle == 64) {
+      if (pool == pool_end && !drained) {  // grab the next chunk (wave-uniform)
+        uint32_t b = 0;
+        if (lane_id() == 0) b = atomicAdd(&ctrl->trace_next, kTraceChunk);
+        b = __shfl(b, 0, 64);
+        pool = b < n ? b : n;
+        pool_end = b + kTraceChunk < n ? b + kTraceChunk : n;
+        drained = b + kTraceChunk >= n;
+      }
+      const uint32_t avail = pool_end - pool;
+      if (ray == 0xFFFFFFFFu) {
+        const uint32_t r = lane_rank(idle);
+        if (r < avail) {
+          ray = MRT_IDX(S, pool + r, n, 20);
+          const float4 o4 = in.ro[ray], d4 = in.rd[ray];
+          trav_init(S, t, V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, tmin, tmax);
+        }
+      }
+      pool += n_idle < avail ? n_idle : avail;
+      if (__ballot(ray != 0xFFFFFFFFu) == 0) break;  // chunk source exhausted
+    }
+    const bool busy = !t.done;  // idle lanes hold a done Trav
+    const bool at_box = busy && trav_at_box(t);
+    const unsigned long long box_mask = __ballot(at_box);
+    const unsigned long long prim_mask = __ballot(busy && !at_box);
+    if (at_box) trav_box<COUNT>(S, t, lc);
+    // primitives wait until enough lanes are at one (or no lane is at a box)
+    if ((__popcll(prim_mask) >= kPrimBatch || box_mask == 0) && busy && !at_box) trav_prim<COUNT>(S, t, lc);
+    if (ray != 0xFFFFFFFFu && t.done) {
+      hits[ray] = make_uint4(__float_as_uint(t.h.t), t.h.prim, t.h.container, 0u);
+      seg += 1;
+      nh += t.h.prim != kRefNone;
+      ray = 0xFFFFFFFFu;
+    }
   }
   if (COUNT) flush_counters(cnt, lc, seg, nh, 0, 0);
+}
+
+// Debug/bisection variant (MRT_RENDER_SIMPLE_TRACE): one ray per thread,
+// the whole traversal in closest_hit.
+__global__ __launch_bounds__(kBlock) void k_trace_simple(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl,
+                                                         uint32_t cur, DevCounters* cnt) {
+  const uint32_t n = ctrl->active[cur];
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = 0;
+  LocalCounters lc;
+  uint32_t seg = 0, nh = 0;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const float4 o4 = in.ro[i], d4 = in.rd[i];
+    Hit h = closest_hit<true>(S, V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, 0.001f, INFINITY, lc);
+    hits[i] = make_uint4(__float_as_uint(h.t), h.prim, h.container, 0u);
+    seg += 1;
+    nh += h.prim != kRefNone;
+  }
+  flush_counters(cnt, lc, seg, nh, 0, 0);
 }
 
 template <bool COUNT>
@@ -147,6 +209,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, DevCamera cam, Ren
                                                   PathBufs out, const uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   float4* results, DevCounters* cnt) {
   const uint32_t n = ctrl->active[cur];
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->trace_next = 0;  // k_trace of the next iteration
   const uint32_t base = blockIdx.x * kBlock;
   if (base >= n) return;
   const uint32_t i = base + threadIdx.x;
@@ -192,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, DevCamera cam, Ren
       rad = make_float4(L.x, L.y, L.z, 0.0f);
       rs = make_uint4((uint32_t)rng.s0, (uint32_t)(rng.s0 >> 32), (uint32_t)rng.s1, (uint32_t)(rng.s1 >> 32));
     } else {
-      results[g] = make_float4(L.x, L.y, L.z, __uint_as_float(k));
+      results[MRT_IDX(S, g, rp.G, 21)] = make_float4(L.x, L.y, L.z, __uint_as_float(k));
       need = true;
       nsample = 1;
     }
@@ -217,7 +280,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, DevCamera cam, Ren
   if (lane_id() == 0 && alive_mask) obase = atomicAdd(&ctrl->active[cur ^ 1], (uint32_t)__popcll(alive_mask));
   obase = __shfl(obase, 0, 64);
   if (alive) {
-    uint32_t pos = obase + lane_rank(alive_mask);
+    uint32_t pos = MRT_IDX(S, obase + lane_rank(alive_mask), rp.pool_cap, 22);
     out.ro[pos] = ro;
     out.rd[pos] = rd;
     out.thr[pos] = thr;
@@ -249,23 +312,27 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(const float4* results, ui
   accum_bounces[p] = k;
 }
 
-// Parity entry point: closest hit of arbitrary rays.
-__global__ __launch_bounds__(kBlock) void k_trace_rays(DevScene S, const float* rays, uint32_t n, float tmin,
-                                                       float tmax, uint4* out, DevCounters* cnt) {
+// mrt_trace_rays: arbitrary rays go through the product k_trace. In: rays
+// (6 floats each) -> pool slots; out: hit records -> mrt_hit with front_face.
+__global__ __launch_bounds__(kBlock) void k_rays_in(const float* rays, uint32_t n, PathBufs out) {
   uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  LocalCounters lc;
-  uint32_t seg = 0, nh = 0;
-  if (i < n) {
-    V3 o{rays[6 * (size_t)i], rays[6 * (size_t)i + 1], rays[6 * (size_t)i + 2]};
-    V3 d{rays[6 * (size_t)i + 3], rays[6 * (size_t)i + 4], rays[6 * (size_t)i + 5]};
-    Hit h = closest_hit<true>(S, o, d, tmin, tmax, lc);
-    uint32_t front = 0;
-    if (h.prim != kRefNone) front = resolve_hit(S, o, d, h).front_face ? 1u : 0u;
-    out[i] = make_uint4(h.prim, h.container, __float_as_uint(h.prim != kRefNone ? h.t : 0.0f), front);
-    seg = 1;
-    nh = h.prim != kRefNone;
-  }
-  flush_counters(cnt, lc, seg, nh, 0, 0);
+  if (i >= n) return;
+  const float* r = rays + 6 * (size_t)i;
+  out.ro[i] = make_float4(r[0], r[1], r[2], __uint_as_float(i));
+  out.rd[i] = make_float4(r[3], r[4], r[5], __uint_as_float(0u));
+}
+
+__global__ __launch_bounds__(kBlock) void k_rays_out(DevScene S, PathBufs in, const uint4* hits, uint32_t n,
+                                                     uint4* out) {
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float4 o4 = in.ro[i], d4 = in.rd[i];
+  const uint4 hv = hits[i];
+  Hit h{__uint_as_float(hv.x), hv.y, hv.z};
+  uint32_t front = 0;
+  if (h.prim != kRefNone)
+    front = resolve_hit(S, V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, h).front_face ? 1u : 0u;
+  out[i] = make_uint4(h.prim, h.container, __float_as_uint(h.prim != kRefNone ? h.t : 0.0f), front);
 }
 
 // div_cr (path.h) against the IEEE division on random bit patterns plus
@@ -355,8 +422,10 @@ struct mrt_ctx {
   size_t results_cap = 0;
   Ctrl* ctrl = nullptr;
   DevCounters* d_cnt = nullptr;
+  uint32_t* dbg = nullptr;  // MRT_DEBUG_BOUNDS record (4 words)
   Ctrl* h_status = nullptr;  // pinned, 2 slots
   hipEvent_t ev[2]{};
+  uint32_t trace_grid = 1024;  // persistent k_trace workgroups (set from the CU count)
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t*, uint32_t>> pixlists;
   // host-buffer render staging
   float* d_acc_rgb = nullptr;
@@ -496,12 +565,13 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
     rp.G = n_pix * cs;
     rp.sample_base = a->spp_begin + done;
     rp.pixlist = pl.first;
+    rp.pool_cap = (uint32_t)c->pool_cap;
     if (a->max_depth == 0) {
       // trace(ray, 0) returns (0, 0) for every sample: nothing to add
       continue;
     }
     uint32_t n0 = (uint32_t)std::min<size_t>(rp.G, c->pool_cap);
-    Ctrl init{{n0, 0}, n0, 0};
+    Ctrl init{{n0, 0}, n0, 0};  // trace_next = 0
     HIP_CHECK(hipMemcpyAsync(c->ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_generate, dim3((n0 + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c->cam, rp, c->bufs[0], n0);
     HIP_CHECK(hipGetLastError());
@@ -528,12 +598,15 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
           m[0] = next_event();
           HIP_CHECK(hipEventRecord(m[0], st));
         }
-        if (count)
-          hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(kBlock), 0, st, c->S, c->bufs[cur], c->hits, c->ctrl,
-                             cur, c->d_cnt);
+        if (a->flags & MRT_RENDER_SIMPLE_TRACE)
+          hipLaunchKernelGGL(k_trace_simple, dim3(c->trace_grid), dim3(kBlock), 0, st, c->S, c->bufs[cur], c->hits,
+                             c->ctrl, cur, c->d_cnt);
+        else if (count)
+          hipLaunchKernelGGL(k_trace<true>, dim3(c->trace_grid), dim3(kBlock), 0, st, c->S, c->bufs[cur], c->hits,
+                             c->ctrl, cur, c->d_cnt, kTmin, INFINITY);
         else
-          hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(kBlock), 0, st, c->S, c->bufs[cur], c->hits, c->ctrl,
-                             cur, c->d_cnt);
+          hipLaunchKernelGGL(k_trace<false>, dim3(c->trace_grid), dim3(kBlock), 0, st, c->S, c->bufs[cur], c->hits,
+                             c->ctrl, cur, c->d_cnt, kTmin, INFINITY);
         HIP_CHECK(hipGetLastError());
         if (timing) {
           m[1] = next_event();
@@ -617,9 +690,14 @@ int mrt_create(int device, mrt_ctx** out) {
     HIP_CHECK(hipMalloc(&c->ctrl, sizeof(Ctrl)));
     HIP_CHECK(hipMalloc(&c->d_cnt, sizeof(DevCounters)));
     HIP_CHECK(hipMemset(c->d_cnt, 0, sizeof(DevCounters)));
+    HIP_CHECK(hipMalloc(&c->dbg, 16));
+    HIP_CHECK(hipMemset(c->dbg, 0, 16));
     HIP_CHECK(hipHostMalloc(&c->h_status, 2 * sizeof(Ctrl), hipHostMallocDefault));
     HIP_CHECK(hipEventCreateWithFlags(&c->ev[0], hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&c->ev[1], hipEventDisableTiming));
+    int cus = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    c->trace_grid = (uint32_t)std::max(1, cus) * 4;  // 4 x 256-thread WGs per CU = 16 waves/CU
   });
   if (rc != MRT_OK) {
     g_last_error = c->err;
@@ -639,6 +717,7 @@ int mrt_destroy(mrt_ctx* c) {
   hipFree(c->results);
   hipFree(c->ctrl);
   hipFree(c->d_cnt);
+  hipFree(c->dbg);
   hipFree(c->d_acc_rgb);
   hipFree(c->d_acc_b);
   hipFree(c->d_rays);
@@ -705,6 +784,15 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     S.textures = (const GpuTexture*)(base + o_tex);
     S.texels = (const uint32_t*)(base + o_texel);
     S.fast_ok = hs.fast_ok;
+    S.n_slots = (uint32_t)(hs.slots.size() / 4);
+    S.n_tris = (uint32_t)(hs.tri_shade.size() / (kTriShadeQuads * 4));
+    S.n_sph = (uint32_t)hs.sph_mat.size();
+    S.n_inst = (uint32_t)hs.inst_mat.size();
+    S.n_models = (uint32_t)hs.model_mat.size();
+    S.n_materials = (uint32_t)hs.materials.size();
+    S.n_textures = (uint32_t)hs.textures.size();
+    S.n_texels = (uint32_t)hs.texels.size();
+    S.dbg = c->dbg;
     S.bg_kind = hs.bg_kind;
     S.bg_texture = hs.bg_texture;
     S.bg_surf_kind = hs.bg_surf_kind;
@@ -782,8 +870,17 @@ int mrt_trace_rays(mrt_ctx* c, const float* rays, uint32_t n, float t_min, float
       c->rays_cap = n;
     }
     HIP_CHECK(hipMemcpyAsync(c->d_rays, rays, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(k_trace_rays, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, c->S,
-                       (const float*)c->d_rays, n, t_min, t_max, c->d_rhits, c->d_cnt);
+    ensure_pool(c, n);
+    const uint32_t g = (n + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_rays_in, dim3(g), dim3(kBlock), 0, c->stream, (const float*)c->d_rays, n, c->bufs[0]);
+    HIP_CHECK(hipGetLastError());
+    Ctrl init{{n, 0}, n, 0};
+    HIP_CHECK(hipMemcpyAsync(c->ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_trace<true>, dim3(c->trace_grid), dim3(kBlock), 0, c->stream, c->S, c->bufs[0], c->hits,
+                       c->ctrl, 0u, c->d_cnt, t_min, t_max);
+    HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_rays_out, dim3(g), dim3(kBlock), 0, c->stream, c->S, c->bufs[0], (const uint4*)c->hits, n,
+                       c->d_rhits);
     HIP_CHECK(hipGetLastError());
     std::vector<uint4> h(n);
     HIP_CHECK(hipMemcpyAsync(h.data(), c->d_rhits, (size_t)n * 16, hipMemcpyDeviceToHost, c->stream));
@@ -843,6 +940,22 @@ int mrt_selftest_division(mrt_ctx* c, uint64_t n, uint64_t seed, uint64_t* misma
     HIP_CHECK(hipFree(d));
     *mismatches = h;
   });
+}
+
+int mrt_debug_status(mrt_ctx* c, uint32_t* out4) {
+  return guarded(c, [&] {
+    if (!out4) throw ApiError{MRT_ERR_INVALID, "null output"};
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipMemcpy(out4, c->dbg, 16, hipMemcpyDeviceToHost));
+  });
+}
+
+int mrt_debug_build(void) {
+#ifdef MRT_DEBUG_BOUNDS
+  return 1;
+#else
+  return 0;
+#endif
 }
 
 int mrt_reset_counters(mrt_ctx* c) {

@@ -18,7 +18,11 @@ from pathlib import Path
 import numpy as np
 
 _HERE = Path(__file__).resolve().parent
-LIB_PATH = _HERE / "libmassrt.so"
+# MASSRT_LIB=dbg selects the bounds-checked debug build (make DEBUG=1); a path
+# ending in .so selects that build (experiments)
+_SEL = os.environ.get("MASSRT_LIB", "")
+LIB_PATH = (Path(_SEL) if _SEL.endswith(".so") else
+            _HERE / ("libmassrt_dbg.so" if _SEL == "dbg" else "libmassrt.so"))
 REPO = _HERE.parent.parent
 
 # ---- constants (massrt.h) --------------------------------------------------
@@ -29,6 +33,7 @@ BG_SOLID, BG_SKY, BG_SKYSPHERE = range(3)
 NO_MATERIAL = 0xFFFFFFFF
 RENDER_COUNTERS = 1
 RENDER_TIME_KERNELS = 2
+RENDER_SIMPLE_TRACE = 4  # debug: one-ray-per-thread closest hit (bisection aid)
 MAX_DEPTH = 50  # main.rs:37
 ASPECT_RATIO = np.float32(16.0) / np.float32(9.0)  # main.rs:39 (f32)
 
@@ -145,7 +150,7 @@ EXPORTED_SYMBOLS = [
     "mrt_create", "mrt_destroy", "mrt_last_error", "mrt_global_last_error", "mrt_abi_version",
     "mrt_upload_scene", "mrt_set_camera", "mrt_render", "mrt_render_device", "mrt_trace_rays",
     "mrt_get_counters", "mrt_reset_counters", "mrt_scene_device_bytes", "mrt_get_kernel_stats",
-    "mrt_reset_kernel_stats", "mrt_selftest_division",
+    "mrt_reset_kernel_stats", "mrt_selftest_division", "mrt_debug_status", "mrt_debug_build",
     "mrt_builder_new", "mrt_builder_free", "mrt_builder_builtin", "mrt_builder_rand_f32", "mrt_builder_solid",
     "mrt_builder_texture_png", "mrt_builder_texture_rgba", "mrt_builder_material", "mrt_builder_background",
     "mrt_builder_add_sphere", "mrt_builder_add_triangle", "mrt_builder_model", "mrt_builder_model_from_ply",
@@ -183,6 +188,8 @@ def lib() -> C.CDLL:
         "mrt_get_kernel_stats": (I, [P, C.POINTER(MrtKernelStats)]),
         "mrt_reset_kernel_stats": (I, [P]),
         "mrt_selftest_division": (I, [P, U64, U64, C.POINTER(C.c_uint64)]),
+        "mrt_debug_status": (I, [P, C.POINTER(C.c_uint32)]),
+        "mrt_debug_build": (I, []),
         "mrt_scene_device_bytes": (I, [P, C.POINTER(C.c_uint64)]),
         "mrt_builder_new": (I, [U64, C.POINTER(P)]),
         "mrt_builder_free": (I, [P]),
@@ -398,19 +405,20 @@ class Context:
 
     @staticmethod
     def args(width, height, spp_begin=0, spp_count=1, seed=1, max_depth=MAX_DEPTH, shard_index=0, shard_count=1,
-             counters=False, time_kernels=False) -> MrtRenderArgs:
-        flags = (RENDER_COUNTERS if counters else 0) | (RENDER_TIME_KERNELS if time_kernels else 0)
+             counters=False, time_kernels=False, flags=0) -> MrtRenderArgs:
+        flags |= (RENDER_COUNTERS if counters else 0) | (RENDER_TIME_KERNELS if time_kernels else 0)
         return MrtRenderArgs(width, height, spp_begin, spp_count, seed, max_depth, shard_index, shard_count, flags)
 
     def render(self, width, height, spp_begin=0, spp_count=1, seed=1, max_depth=MAX_DEPTH, shard_index=0,
-               shard_count=1, counters=False, accum=None):
+               shard_count=1, counters=False, accum=None, flags=0):
         """Returns (rgb float32 [H*W*3], bounces uint32 [H*W]) accumulated in sample order."""
         if accum is None:
             rgb = np.zeros(width * height * 3, dtype=np.float32)
             b = np.zeros(width * height, dtype=np.uint32)
         else:
             rgb, b = accum
-        a = self.args(width, height, spp_begin, spp_count, seed, max_depth, shard_index, shard_count, counters)
+        a = self.args(width, height, spp_begin, spp_count, seed, max_depth, shard_index, shard_count, counters,
+                      flags=flags)
         self._check(lib().mrt_render(self.h, C.byref(a), _fptr(rgb), b.ctypes.data_as(C.POINTER(C.c_uint32))))
         return rgb, b
 
@@ -443,6 +451,11 @@ class Context:
         m = C.c_uint64()
         self._check(lib().mrt_selftest_division(self.h, n, seed, C.byref(m)))
         return int(m.value)
+
+    def debug_status(self):
+        out = (C.c_uint32 * 4)()
+        self._check(lib().mrt_debug_status(self.h, out))
+        return list(out)
 
     def reset_kernel_stats(self):
         self._check(lib().mrt_reset_kernel_stats(self.h))

@@ -224,6 +224,54 @@ def test_backgrounds_textures_and_alpha(ctx):
         assert oc["alpha_taps"] > 0
 
 
+def _alpha_plane(rng):
+    tex = rng.integers(0, 256, size=(16, 24, 4), dtype=np.uint8)
+    tex[..., 3] = np.where(rng.random((16, 24)) < 0.3, 0, 255)
+    grid = np.linspace(-2, 2, 9, dtype=np.float32)
+    tris = []
+    for i in range(8):
+        for j in range(8):
+            x0, x1, y0, y1 = grid[i], grid[i + 1], grid[j], grid[j + 1]
+            for tri in ([[x0, y0, 0], [x1, y0, 0], [x1, y1, 0]], [[x0, y0, 0], [x1, y1, 0], [x0, y1, 0]]):
+                row = []
+                for v in tri:
+                    row += list(v) + [0, 0, 1] + [v[0] * 0.3 + 0.5, v[1] * 0.3 + 0.5]
+                tris.append(row)
+    return tex, np.array(tris, dtype=np.float32)
+
+
+@pytest.mark.parametrize("variant", ["model", "instance", "both"])
+def test_trace_rays_model_blas_random(ctx, variant):
+    """Random rays in and around an alpha-textured mesh reached through a
+    world-level Model and/or an Instance (geom.rs:318-326, 405-419). This is
+    the regression test for the SLP-vectoriser miscompile of k_trace (Makefile):
+    with it, rays entering the model BLAS lost every hit."""
+    tex, tris = _alpha_plane(np.random.default_rng(7))
+
+    def scene(x):
+        st = x.texture_rgba(tex, massrt.WRAP_REPEAT)
+        x.background(massrt.BG_SKY)
+        mt = x.material(massrt.MAT_LAMBERTIAN, st)
+        m = x.model(mt, tris, add_to_world=variant in ("model", "both"), shading=True)
+        if variant in ("instance", "both"):
+            x.add_instance(m, (0.5, 0.2, -1.5), (0.1, 0.2, 0.05), (1.2, 0.8, 1.0), x.material(massrt.MAT_METAL, st, 0.3))
+        x.add_sphere(x.material(massrt.MAT_DIELECTRIC, 0, 1.4), (0.3, 0.1, 1.0), 0.5)
+        x.build_bvh()
+        x.camera(45.0, (0.5, 0.8, 6), (0, 0, 0), aspect=ASPECT)
+
+    b, o = build_both(scene)
+    ctx.upload(b)
+    r = np.random.default_rng(3)
+    rays = np.concatenate([r.uniform(-2.5, 2.5, (100_000, 3)), r.normal(size=(100_000, 3))], 1).astype(np.float32)
+    g, ob = ctx.trace_rays(rays), o.trace_rays(rays)
+    assert (ob[:, 1] >> 28 != 0).sum() > 5_000  # many hits inside a BLAS
+    assert np.array_equal(g, ob)
+    # the one-ray-per-thread debug kernel renders the same image
+    rgb, bo = ctx.render(32, 18, 0, 2, seed=5)
+    rgb2, bo2 = ctx.render(32, 18, 0, 2, seed=5, flags=massrt.RENDER_SIMPLE_TRACE)
+    assert np.array_equal(bo, bo2) and np.array_equal(rgb, rgb2)
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_random_worlds_with_ties(ctx, seed):
     from test_bvh import random_world
