@@ -7,8 +7,10 @@ A step = one pass of the hot path over one batch: `--spp-per-step` samples
 (default 64) of every pixel of the 1920x1080 frame; 16 steps = the full
 1024-spp config. With N GPUs (torchrun, one rank per GPU, RCCL over xGMI)
 each rank renders every N-th 8x8 framebuffer tile of the same frame (strong
-scaling) and the per-step tile buffers are summed onto rank 0 with one
-dist.reduce (Image::merge, main.rs:629-638); no other exchange exists.
+scaling), accumulating its tiles in its own HBM frame, and after every step
+the per-rank frames are summed onto rank 0 with one dist.reduce
+(massrt/shard.py; Image::merge, main.rs:629-638) — bit-identical to the
+1-GPU image; no other exchange exists.
 
 Inputs (scene, BVH, camera) are resident in HBM before timing; the
 accumulation buffers live in HBM. `value` = all samples of all ranks / the
@@ -60,6 +62,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--pmc-json", default=None, help="PMC summary (default profiles/pmc_<scene>.json)")
     return ap.parse_args()
 
@@ -106,14 +109,15 @@ def main():
     import torch.distributed as dist
 
     import massrt
+    from massrt.shard import ShardedFrame
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group(a.dist_backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -122,31 +126,21 @@ def main():
     ctx = massrt.Context(torch.cuda.current_device())
     b = massrt.Builder(1).builtin(a.scene, float(massrt.ASPECT_RATIO), str(asset_dir(a.scene)))
     ctx.upload(b)
-    frame_rgb = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
-    frame_b = torch.zeros(W * H, dtype=torch.int32, device=dev)
-    step_rgb = torch.zeros_like(frame_rgb) if world > 1 else frame_rgb
-    step_b = torch.zeros_like(frame_b) if world > 1 else frame_b
+    frame = ShardedFrame(W, H, dev, rank, world)
     stream = torch.cuda.current_stream().cuda_stream
 
-    def step(k: int, counters=False, timing=False):
-        if world > 1:
-            step_rgb.zero_()
-            step_b.zero_()
-        args = ctx.args(W, H, k * spp, spp, a.seed, a.max_depth, rank, world, counters=counters,
-                        time_kernels=timing)
-        ctx.render_device(args, step_rgb.data_ptr(), step_b.data_ptr(), stream)
-        if world > 1:
-            dist.reduce(step_rgb, 0)
-            dist.reduce(step_b, 0)
-            if rank == 0:
-                frame_rgb.add_(step_rgb)
-                frame_b.add_(step_b)
+    def step(counters=False, timing=False):
+        def render_into(rgb, bounces, s0, n):
+            args = ctx.args(W, H, s0, n, a.seed, a.max_depth, rank, world, counters=counters, time_kernels=timing)
+            ctx.render_device(args, rgb.data_ptr(), bounces.data_ptr(), stream)
+
+        frame.step(render_into, spp)  # renders this rank's tiles, then one reduce onto rank 0
 
     # warmup; the first warmup step also counts traversal events (statistics
     # for the algorithmic-bytes model — not part of the timed region)
     ctx.reset_counters()
     for k in range(a.warmup):
-        step(k, counters=(k == 0))
+        step(counters=(k == 0))
     torch.cuda.synchronize()
     cnt = ctx.counters()
     ctx.reset_kernel_stats()
@@ -156,8 +150,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(a.warmup, a.warmup + a.steps):
-        step(k, timing=timing)
+    for _ in range(a.steps):
+        step(timing=timing)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -206,7 +200,7 @@ def main():
             cpu = {"value": None, "error": str(e)}
 
     if rank == 0:
-        mean_bounces = float(frame_b.double().sum().item()) / (W * H * spp * (a.steps + a.warmup))
+        mean_bounces = float(frame.frame()[1].double().sum().item()) / (W * H * spp * (a.steps + a.warmup))
         line = {
             "metric": METRIC,
             "value": round(value, 3),

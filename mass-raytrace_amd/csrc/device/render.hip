@@ -84,6 +84,28 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
+constexpr uint32_t kWaves = kBlock / 64;
+
+// Workgroup-wide reservation of `count` (this wave's share) consecutive
+// slots from *counter: one atomic per workgroup; returns this wave's first
+// slot. Every thread of the workgroup must call it.
+__device__ __forceinline__ uint32_t wg_reserve(uint32_t* counter, uint32_t count, uint32_t wave, uint32_t* s_cnt,
+                                               uint32_t& s_base) {
+  if (lane_id() == 0) s_cnt[wave] = count;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t total = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kWaves; ++w) total += s_cnt[w];
+    s_base = total ? atomicAdd(counter, total) : 0u;
+  }
+  __syncthreads();
+  uint32_t base = s_base;
+  for (uint32_t w = 0; w < wave; ++w) base += s_cnt[w];
+  __syncthreads();  // s_cnt/s_base are reused by the next call
+  return base;
+}
+
 __device__ void flush_counters(DevCounters* c, const LocalCounters& lc, uint32_t segs, uint32_t hits,
                                uint32_t samples, uint32_t bounces) {
   uint32_t v[10] = {samples, segs, lc.node_visits, lc.sphere_tests, lc.triangle_tests, lc.instance_entries,
@@ -260,11 +282,13 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, DevCamera cam, Ren
       nsample = 1;
     }
   }
-  // regenerate finished slots from the work counter (one atomic per wave)
+  // regenerate finished slots from the work counter and compact survivors
+  // into the next pool: one atomic per workgroup for each (same-address
+  // atomics from every wave serialise in L2)
+  __shared__ uint32_t s_cnt[kWaves], s_base;
+  const uint32_t wave = threadIdx.x / 64;
   const unsigned long long need_mask = __ballot(need);
-  uint32_t wbase = 0;
-  if (lane_id() == 0 && need_mask) wbase = atomicAdd(&ctrl->next_work, (uint32_t)__popcll(need_mask));
-  wbase = __shfl(wbase, 0, 64);
+  const uint32_t wbase = wg_reserve(&ctrl->next_work, (uint32_t)__popcll(need_mask), wave, s_cnt, s_base);
   if (need) {
     uint32_t g = wbase + lane_rank(need_mask);
     if (g < rp.G) {
@@ -276,9 +300,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, DevCamera cam, Ren
   }
   // compact survivors + new paths into the next pool
   const unsigned long long alive_mask = __ballot(alive);
-  uint32_t obase = 0;
-  if (lane_id() == 0 && alive_mask) obase = atomicAdd(&ctrl->active[cur ^ 1], (uint32_t)__popcll(alive_mask));
-  obase = __shfl(obase, 0, 64);
+  const uint32_t obase = wg_reserve(&ctrl->active[cur ^ 1], (uint32_t)__popcll(alive_mask), wave, s_cnt, s_base);
   if (alive) {
     uint32_t pos = MRT_IDX(S, obase + lane_rank(alive_mask), rp.pool_cap, 22);
     out.ro[pos] = ro;
@@ -697,7 +719,12 @@ int mrt_create(int device, mrt_ctx** out) {
     HIP_CHECK(hipEventCreateWithFlags(&c->ev[1], hipEventDisableTiming));
     int cus = 0;
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-    c->trace_grid = (uint32_t)std::max(1, cus) * 4;  // 4 x 256-thread WGs per CU = 16 waves/CU
+    // persistent k_trace: as many resident workgroups as the register budget
+    // allows on every CU (MRT_TRACE_WGS_PER_CU overrides, for tuning)
+    int per_cu = 0;
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false>, kBlock, 0));
+    if (const char* e = getenv("MRT_TRACE_WGS_PER_CU")) per_cu = atoi(e);
+    c->trace_grid = (uint32_t)std::max(1, cus) * (uint32_t)std::max(1, per_cu);
   });
   if (rc != MRT_OK) {
     g_last_error = c->err;
