@@ -338,7 +338,7 @@ MRT_DEV bool box_hit_any(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) {
 }
 
 // Move to record t.i (leaving a finished BLAS region) and prefetch it.
-MRT_DEV void trav_fetch(const DevScene& S, Trav& t) {
+MRT_DEV void trav_fetch(const DevScene& S, const uint4* slots, Trav& t) {
   if (t.i >= t.end) {
     if (t.ret == 0xFFFFFFFFu) {
       t.done = true;
@@ -354,7 +354,6 @@ MRT_DEV void trav_fetch(const DevScene& S, Trav& t) {
       return;
     }
   }
-  const uint4* slots = reinterpret_cast<const uint4*>(S.slots);
 #ifdef MRT_DEBUG_BOUNDS
   if (t.i + 1 >= S.n_slots || ++t.steps > (1u << 24)) {  // record and stop instead of looping/faulting
     MRT_IDX(S, t.i + 1 >= S.n_slots ? t.i : 0xFFFFFFF0u, t.i + 1 >= S.n_slots ? S.n_slots : 0u, 5);
@@ -366,7 +365,7 @@ MRT_DEV void trav_fetch(const DevScene& S, Trav& t) {
   t.s1 = slots[MRT_IDX(S, t.i + 1, S.n_slots, 6)];
 }
 
-MRT_DEV void trav_init(const DevScene& S, Trav& t, V3 o, V3 d, float tmin, float tmax) {
+MRT_DEV void trav_init(const DevScene& S, const uint4* slots, Trav& t, V3 o, V3 d, float tmin, float tmax) {
   t.world = make_tray(o, d, S.fast_ok);
   t.r = t.world;
   t.i = S.world_begin;
@@ -380,28 +379,28 @@ MRT_DEV void trav_init(const DevScene& S, Trav& t, V3 o, V3 d, float tmin, float
 #ifdef MRT_DEBUG_BOUNDS
   t.steps = 0;
 #endif
-  trav_fetch(S, t);
+  trav_fetch(S, slots, t);
 }
 
 MRT_DEV bool trav_at_box(const Trav& t) { return t.s1.w == KIND_BOX; }
 
 // The current record is a box: test it and move on.
 template <bool COUNT>
-MRT_DEV void trav_box(const DevScene& S, Trav& t, LocalCounters& lc) {
+MRT_DEV void trav_box(const DevScene& S, const uint4* slots, Trav& t, LocalCounters& lc) {
   if (COUNT) lc.node_visits++;
   V3 mn{u2f(t.s0.x), u2f(t.s0.y), u2f(t.s0.z)}, mx{u2f(t.s0.w), u2f(t.s1.x), u2f(t.s1.y)};
   t.i = box_hit_any(mn, mx, t.r, t.tmin, t.best) ? t.i + 2 : t.s1.z;
-  trav_fetch(S, t);
+  trav_fetch(S, slots, t);
 }
 
 // The current record is a primitive, an instance or a model.
 template <bool COUNT>
-MRT_DEV void trav_prim(const DevScene& S, Trav& t, LocalCounters& lc) {
+MRT_DEV void trav_prim(const DevScene& S, const uint4* slots, Trav& t, LocalCounters& lc) {
   const uint4 s0 = t.s0, s1 = t.s1;
   const uint32_t kind = s1.w;
   if (kind == KIND_TRI) {
     if (COUNT) lc.triangle_tests++;
-    const uint4 s2 = reinterpret_cast<const uint4*>(S.slots)[MRT_IDX(S, t.i + 2, S.n_slots, 7)];
+    const uint4 s2 = slots[MRT_IDX(S, t.i + 2, S.n_slots, 7)];
     V3 a{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, ab{u2f(s0.w), u2f(s1.x), u2f(s1.y)}, ac{u2f(s2.x), u2f(s2.y), u2f(s2.z)};
     float th;
     if (tri_hit(a, ab, ac, t.r.o, t.r.d, t.tmin, t.best, th)) {
@@ -435,18 +434,19 @@ MRT_DEV void trav_prim(const DevScene& S, Trav& t, LocalCounters& lc) {
     t.i = s0.y;
     t.end = s0.z;
   }
-  trav_fetch(S, t);
+  trav_fetch(S, slots, t);
 }
 
 template <bool COUNT>
 MRT_DEV Hit closest_hit(const DevScene& S, V3 o, V3 d, float tmin, float tmax, LocalCounters& lc) {
   Trav t;
-  trav_init(S, t, o, d, tmin, tmax);
+  const uint4* slots = reinterpret_cast<const uint4*>(S.slots);
+  trav_init(S, slots, t, o, d, tmin, tmax);
   while (!t.done) {
     if (trav_at_box(t))
-      trav_box<COUNT>(S, t, lc);
+      trav_box<COUNT>(S, slots, t, lc);
     else
-      trav_prim<COUNT>(S, t, lc);
+      trav_prim<COUNT>(S, slots, t, lc);
   }
   return t.h;
 }

@@ -154,12 +154,24 @@ constexpr uint32_t kTraceChunk = 256;  // rays per atomic grab
 constexpr uint32_t kRefill = 16;       // refill once this many lanes idle
 constexpr uint32_t kPrimBatch = 8;     // run the primitive branch once this many lanes wait at one
 
-template <bool COUNT>
+// LDS=true: the whole record stream is first copied into the workgroup's LDS
+// (scenes up to kTraceLdsMaxBytes, e.g. SphereGrid's ~31 KB), so every
+// traversal step reads LDS instead of L1/L2.
+constexpr size_t kTraceLdsMaxBytes = 64 * 1024;
+
+template <bool COUNT, bool LDS>
 __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   DevCounters* cnt, float tmin, float tmax) {
+  extern __shared__ uint4 lds_slots[];
   const uint32_t n = ctrl->active[cur];
   if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = 0;
-  if (n == 0) return;
+  if (n == 0) return;  // uniform: every workgroup reads the same n
+  const uint4* gslots = reinterpret_cast<const uint4*>(S.slots);
+  if (LDS) {
+    for (uint32_t k = threadIdx.x; k < S.n_slots; k += kBlock) lds_slots[k] = gslots[k];
+    __syncthreads();
+  }
+  const uint4* slots = LDS ? lds_slots : gslots;
   LocalCounters lc;
   uint32_t seg = 0, nh = 0;
   uint32_t pool = 0, pool_end = 0;  // wave-uniform chunk [pool, pool_end)
@@ -185,7 +197,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
         if (r < avail) {
           ray = MRT_IDX(S, pool + r, n, 20);
           const float4 o4 = in.ro[ray], d4 = in.rd[ray];
-          trav_init(S, t, V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, tmin, tmax);
+          trav_init(S, slots, t, V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, tmin, tmax);
         }
       }
       pool += n_idle < avail ? n_idle : avail;
@@ -195,9 +207,9 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
     const bool at_box = busy && trav_at_box(t);
     const unsigned long long box_mask = __ballot(at_box);
     const unsigned long long prim_mask = __ballot(busy && !at_box);
-    if (at_box) trav_box<COUNT>(S, t, lc);
+    if (at_box) trav_box<COUNT>(S, slots, t, lc);
     // primitives wait until enough lanes are at one (or no lane is at a box)
-    if ((__popcll(prim_mask) >= kPrimBatch || box_mask == 0) && busy && !at_box) trav_prim<COUNT>(S, t, lc);
+    if ((__popcll(prim_mask) >= kPrimBatch || box_mask == 0) && busy && !at_box) trav_prim<COUNT>(S, slots, t, lc);
     if (ray != 0xFFFFFFFFu && t.done) {
       hits[ray] = make_uint4(__float_as_uint(t.h.t), t.h.prim, t.h.container, 0u);
       seg += 1;
@@ -448,6 +460,9 @@ struct mrt_ctx {
   Ctrl* h_status = nullptr;  // pinned, 2 slots
   hipEvent_t ev[2]{};
   uint32_t trace_grid = 1024;  // persistent k_trace workgroups (set from the CU count)
+  int cus = 1;
+  bool trace_lds = false;          // record stream staged in LDS (set per scene)
+  uint32_t trace_grid_lds = 1024;  // workgroups of the LDS variant
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t*, uint32_t>> pixlists;
   // host-buffer render staging
   float* d_acc_rgb = nullptr;
@@ -498,6 +513,29 @@ int guarded(mrt_ctx* c, F&& f) {
 template <typename T>
 size_t align_up(size_t x) {
   return (x + 255) & ~(size_t)255;
+}
+
+// The persistent closest-hit kernel over pool buffer `in` (LDS variant when
+// the scene's record stream fits).
+void launch_trace(mrt_ctx* c, hipStream_t st, const PathBufs& in, uint32_t cur, bool count, float tmin, float tmax) {
+  const DevScene& S = c->S;
+  if (c->trace_lds) {
+    const size_t smem = (size_t)S.n_slots * 16;
+    if (count)
+      hipLaunchKernelGGL((k_trace<true, true>), dim3(c->trace_grid_lds), dim3(kBlock), smem, st, S, in, c->hits,
+                         c->ctrl, cur, c->d_cnt, tmin, tmax);
+    else
+      hipLaunchKernelGGL((k_trace<false, true>), dim3(c->trace_grid_lds), dim3(kBlock), smem, st, S, in, c->hits,
+                         c->ctrl, cur, c->d_cnt, tmin, tmax);
+  } else {
+    if (count)
+      hipLaunchKernelGGL((k_trace<true, false>), dim3(c->trace_grid), dim3(kBlock), 0, st, S, in, c->hits, c->ctrl,
+                         cur, c->d_cnt, tmin, tmax);
+    else
+      hipLaunchKernelGGL((k_trace<false, false>), dim3(c->trace_grid), dim3(kBlock), 0, st, S, in, c->hits, c->ctrl,
+                         cur, c->d_cnt, tmin, tmax);
+  }
+  HIP_CHECK(hipGetLastError());
 }
 
 void ensure_pool(mrt_ctx* c, size_t P) {
@@ -623,12 +661,8 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
         if (a->flags & MRT_RENDER_SIMPLE_TRACE)
           hipLaunchKernelGGL(k_trace_simple, dim3(c->trace_grid), dim3(kBlock), 0, st, c->S, c->bufs[cur], c->hits,
                              c->ctrl, cur, c->d_cnt);
-        else if (count)
-          hipLaunchKernelGGL(k_trace<true>, dim3(c->trace_grid), dim3(kBlock), 0, st, c->S, c->bufs[cur], c->hits,
-                             c->ctrl, cur, c->d_cnt, kTmin, INFINITY);
         else
-          hipLaunchKernelGGL(k_trace<false>, dim3(c->trace_grid), dim3(kBlock), 0, st, c->S, c->bufs[cur], c->hits,
-                             c->ctrl, cur, c->d_cnt, kTmin, INFINITY);
+          launch_trace(c, st, c->bufs[cur], cur, count, kTmin, INFINITY);
         HIP_CHECK(hipGetLastError());
         if (timing) {
           m[1] = next_event();
@@ -722,9 +756,12 @@ int mrt_create(int device, mrt_ctx** out) {
     // persistent k_trace: as many resident workgroups as the register budget
     // allows on every CU (MRT_TRACE_WGS_PER_CU overrides, for tuning)
     int per_cu = 0;
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false>, kBlock, 0));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false>, kBlock, 0));
     if (const char* e = getenv("MRT_TRACE_WGS_PER_CU")) per_cu = atoi(e);
-    c->trace_grid = (uint32_t)std::max(1, cus) * (uint32_t)std::max(1, per_cu);
+    c->cus = std::max(1, cus);
+    c->trace_grid = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
+    for (auto f : {(const void*)k_trace<false, true>, (const void*)k_trace<true, true>})
+      HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTraceLdsMaxBytes));
   });
   if (rc != MRT_OK) {
     g_last_error = c->err;
@@ -826,6 +863,14 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     for (int k = 0; k < 4; ++k) S.bg_color[k] = hs.bg_color[k];
     c->S = S;
     c->scene_bytes = off;
+    const size_t lds_bytes = (size_t)S.n_slots * 16;
+    const char* no_lds = getenv("MRT_TRACE_LDS");
+    c->trace_lds = lds_bytes <= kTraceLdsMaxBytes && !(no_lds && no_lds[0] == '0');
+    if (c->trace_lds) {
+      int per_cu = 0;
+      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, true>, kBlock, lds_bytes));
+      c->trace_grid_lds = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
+    }
     c->has_scene = true;
   });
 }
@@ -903,8 +948,7 @@ int mrt_trace_rays(mrt_ctx* c, const float* rays, uint32_t n, float t_min, float
     HIP_CHECK(hipGetLastError());
     Ctrl init{{n, 0}, n, 0};
     HIP_CHECK(hipMemcpyAsync(c->ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(k_trace<true>, dim3(c->trace_grid), dim3(kBlock), 0, c->stream, c->S, c->bufs[0], c->hits,
-                       c->ctrl, 0u, c->d_cnt, t_min, t_max);
+    launch_trace(c, c->stream, c->bufs[0], 0u, true, t_min, t_max);
     HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_rays_out, dim3(g), dim3(kBlock), 0, c->stream, c->S, c->bufs[0], (const uint4*)c->hits, n,
                        c->d_rhits);
