@@ -242,6 +242,11 @@ int mrt_get_kernel_stats(mrt_ctx* ctx, mrt_kernel_stats* out);
 /* Self-test of the device's correctly rounded division (box slab test):
  * n random/structured operand pairs vs IEEE a/b; mismatches must be 0. */
 int mrt_selftest_division(mrt_ctx* ctx, uint64_t n, uint64_t seed, uint64_t* mismatches);
+/* Self-test of the slab test's early decision (approximate quotients with an
+ * error margin, exact fallback near ties) against the exact slab test on n
+ * random rays/boxes built to graze each other; mismatches must be 0,
+ * near_ties counts the cases the exact fallback decided. */
+int mrt_selftest_slab(mrt_ctx* ctx, uint64_t n, uint64_t seed, uint64_t* mismatches, uint64_t* near_ties);
 /* Debug builds (-DMRT_DEBUG_BOUNDS, libmassrt_dbg.so) check every scene and
  * path-buffer index on the device and record the first failure here as
  * {check code, index, bound, failure count} instead of faulting.

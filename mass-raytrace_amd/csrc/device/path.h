@@ -112,15 +112,15 @@ MRT_DEV V4 surface_get_f(const DevScene& S, const GpuMaterial& m, V2 uv, LocalCo
 // bit-exact against `a / b` by mrt_selftest_division.
 struct Recip {
   float b, y;
-  bool ok;
 };
 MRT_DEV Recip make_recip(float b) {
   Recip r;
   r.b = b;
   r.y = 1.0f / b;
-  r.ok = fabsf(b) >= 0x1p-60f && fabsf(b) <= 0x1p60f;
   return r;
 }
+// divisor inside the fast path's range
+MRT_DEV bool recip_ok(const Recip& r) { return fabsf(r.b) >= 0x1p-60f && fabsf(r.b) <= 0x1p60f; }
 // q ~ RN(a/b): exact whenever div_in_range(q, a) and the divisor was `ok`
 MRT_DEV float div_fast(float a, const Recip& r) {
   float q = a * r.y;
@@ -137,7 +137,7 @@ MRT_DEV bool div_in_range(float q, float a) {
 }
 MRT_DEV float div_cr(float a, const Recip& r) {
   float q = div_fast(a, r);
-  if (!r.ok || !div_in_range(q, a)) q = a / r.b;
+  if (!recip_ok(r) || !div_in_range(q, a)) q = a / r.b;
   return q;
 }
 // Ray in the space being traversed (world, or an instance's object space)
@@ -277,23 +277,52 @@ struct Hit {
   uint32_t container;  // make_ref(INSTANCE|MODEL, id) or kRefNone
 };
 
-// World::intersect(ray, t_min, t_max) over the preorder stream.
 // World::intersect over the preorder stream, one record per step so that a
 // persistent kernel can interleave many rays per lane (render.hip k_trace).
 // Each lane's sequence of box/primitive tests is exactly the reference's
 // (left-first recursion with shrinking t_max, geom.rs:185-205); only which
 // lanes of a wave are busy at a time differs.
+//
+// Register budget: the per-lane state is kept small (occupancy is the lever
+// for this latency-bound loop). The world ray is not kept: the rays live in
+// the pool buffers (ro/rd), and leaving an instance's BLAS reloads it. The
+// closest t so far is `best` (Hit.t is filled in by trav_hit()).
+struct TravIn {
+  const DevScene& S;
+  const uint4* slots;      // record stream (global, or its LDS copy)
+  const float4* ro;        // ray origins  (xyz) of the pool
+  const float4* rd;        // ray directions (xyz)
+  float tmin;
+};
+
+// Inside a BLAS, `ret` is the world record after the instance/model record
+// that entered it, with kRetInstance set for an instance; the container of a
+// hit is recovered from that record when the ray finishes (trav_hit).
+constexpr uint32_t kNoRet = 0xFFFFFFFFu;
+constexpr uint32_t kRetInstance = 0x80000000u;
+
 struct Trav {
-  TRay world, r;  // world ray, ray of the space being traversed
-  uint32_t i, end, ret, container;
-  float tmin, best;
-  Hit h;
+  TRay r;  // ray of the space being traversed (world, or instance object space)
+  uint32_t ray;  // pool index of the ray
+  uint32_t i, end, ret;
+  float best;
+  uint32_t prim, hit_ret;  // closest hit so far: primitive (kRefNone: none) and `ret` when found
   uint4 s0, s1;  // current record (prefetched when i moves)
   bool done;
 #ifdef MRT_DEBUG_BOUNDS
   uint32_t steps;
 #endif
 };
+
+MRT_DEV Hit trav_hit(const TravIn& in, const Trav& t) {
+  uint32_t container = kRefNone;
+  if (t.hit_ret != kNoRet) {
+    const uint32_t rec = (t.hit_ret & ~kRetInstance) - 2;  // the instance/model record
+    container = make_ref((t.hit_ret & kRetInstance) ? MRT_REF_INSTANCE : MRT_REF_MODEL,
+                         in.slots[MRT_IDX(in.S, rec, in.S.n_slots, 11)].x);
+  }
+  return Hit{t.best, t.prim, container};
+}
 
 // f32 min/max without the canonicalising v_max hipcc inserts before fminf:
 // every operand here is an arithmetic result (never a signalling NaN), for
@@ -324,7 +353,7 @@ MRT_DEV float vmax3(float a, float b, float c) {
 // to IEEE division there), IEEE division otherwise. The per-axis early-outs
 // cannot change the result (t0 only grows, t1 only shrinks, NaNs are ignored
 // by min/max): one final compare of max(tmin, lo) against min(tmax, hi).
-MRT_DEV bool box_hit_any(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) {
+MRT_DEV bool box_hit_exact(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) {
   V3 na = mn - r.o, nb = mx - r.o;
   V3 a{qfast(na.x, r.d.x, r.yx), qfast(na.y, r.d.y, r.yy), qfast(na.z, r.d.z, r.yz)};
   V3 b{qfast(nb.x, r.d.x, r.yx), qfast(nb.y, r.d.y, r.yy), qfast(nb.z, r.d.z, r.yz)};
@@ -337,18 +366,47 @@ MRT_DEV bool box_hit_any(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) {
   return !(t1 < t0);
 }
 
+// The same decision, cheaper: in the fast domain each product (m - o)*RN(1/d)
+// is within 2^-21.9 (relative) of the correctly rounded quotient (one rounding
+// in RN(1/d), one in the product, half an ulp to RN(a/d)); min/max keep that
+// bound for t0 and t1 (relative to their own magnitude). When t1 and t0 are
+// further apart than (|t0|+|t1|)*2^-19 the comparison of the exact values is
+// decided; otherwise — grazing rays, flat boxes, ties — box_hit_exact decides.
+// mrt_selftest_slab checks this against box_hit_exact on near-tie boxes.
+MRT_DEV bool box_hit_any(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) {
+  if (r.fast) {
+    V3 na = mn - r.o, nb = mx - r.o;
+    const float ax = na.x * r.yx, ay = na.y * r.yy, az = na.z * r.yz;
+    const float bx = nb.x * r.yx, by = nb.y * r.yy, bz = nb.z * r.yz;
+    const float t0 = vmax3(vmin1(ax, bx), vmin1(ay, by), vmax1(vmin1(az, bz), tmin));
+    const float t1 = vmin3(vmax1(ax, bx), vmax1(ay, by), vmin1(vmax1(az, bz), tmax));
+    const float m = (fabsf(t0) + fabsf(t1)) * 0x1p-19f;
+    const float gap = t1 - t0;
+    if (gap > m) return true;
+    if (-gap > m) return false;
+  }
+  return box_hit_exact(mn, mx, r, tmin, tmax);
+}
+
+MRT_DEV TRay world_ray(const TravIn& in, uint32_t ray) {
+  const float4 o4 = in.ro[ray], d4 = in.rd[ray];
+  return make_tray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, in.S.fast_ok);
+}
+
 // Move to record t.i (leaving a finished BLAS region) and prefetch it.
-MRT_DEV void trav_fetch(const DevScene& S, const uint4* slots, Trav& t) {
+MRT_DEV void trav_fetch(const TravIn& in, Trav& t) {
+  const DevScene& S = in.S;
   if (t.i >= t.end) {
-    if (t.ret == 0xFFFFFFFFu) {
+    if (t.ret == kNoRet) {
       t.done = true;
       return;
     }
-    t.i = t.ret;  // leave the BLAS: back to the world ray (geom.rs:405-409)
+    // leave the BLAS: back to the world ray (geom.rs:405-409); a model
+    // shares the world ray, an instance's object-space ray is replaced
+    if (t.ret & kRetInstance) t.r = world_ray(in, t.ray);
+    t.i = t.ret & ~kRetInstance;
     t.end = S.world_end;
-    t.ret = 0xFFFFFFFFu;
-    t.r = t.world;
-    t.container = kRefNone;
+    t.ret = kNoRet;
     if (t.i >= t.end) {
       t.done = true;
       return;
@@ -361,94 +419,98 @@ MRT_DEV void trav_fetch(const DevScene& S, const uint4* slots, Trav& t) {
     return;
   }
 #endif
-  t.s0 = slots[MRT_IDX(S, t.i, S.n_slots, 5)];
-  t.s1 = slots[MRT_IDX(S, t.i + 1, S.n_slots, 6)];
+  t.s0 = in.slots[MRT_IDX(S, t.i, S.n_slots, 5)];
+  t.s1 = in.slots[MRT_IDX(S, t.i + 1, S.n_slots, 6)];
 }
 
-MRT_DEV void trav_init(const DevScene& S, const uint4* slots, Trav& t, V3 o, V3 d, float tmin, float tmax) {
-  t.world = make_tray(o, d, S.fast_ok);
-  t.r = t.world;
-  t.i = S.world_begin;
-  t.end = S.world_end;
-  t.ret = 0xFFFFFFFFu;
-  t.container = kRefNone;
-  t.tmin = tmin;
+// Start ray `ray` of the pool (World::intersect(ray, in.tmin, tmax)).
+MRT_DEV void trav_init(const TravIn& in, Trav& t, uint32_t ray, float tmax) {
+  t.r = world_ray(in, ray);
+  t.ray = ray;
+  t.i = in.S.world_begin;
+  t.end = in.S.world_end;
+  t.ret = kNoRet;
   t.best = tmax;
-  t.h = Hit{tmax, kRefNone, kRefNone};
+  t.prim = kRefNone;
+  t.hit_ret = kNoRet;
   t.done = false;
 #ifdef MRT_DEBUG_BOUNDS
   t.steps = 0;
 #endif
-  trav_fetch(S, slots, t);
+  trav_fetch(in, t);
 }
 
 MRT_DEV bool trav_at_box(const Trav& t) { return t.s1.w == KIND_BOX; }
 
 // The current record is a box: test it and move on.
 template <bool COUNT>
-MRT_DEV void trav_box(const DevScene& S, const uint4* slots, Trav& t, LocalCounters& lc) {
+MRT_DEV void trav_box(const TravIn& in, Trav& t, LocalCounters& lc) {
   if (COUNT) lc.node_visits++;
   V3 mn{u2f(t.s0.x), u2f(t.s0.y), u2f(t.s0.z)}, mx{u2f(t.s0.w), u2f(t.s1.x), u2f(t.s1.y)};
-  t.i = box_hit_any(mn, mx, t.r, t.tmin, t.best) ? t.i + 2 : t.s1.z;
-  trav_fetch(S, slots, t);
+  t.i = box_hit_any(mn, mx, t.r, in.tmin, t.best) ? t.i + 2 : t.s1.z;
+  trav_fetch(in, t);
 }
 
-// The current record is a primitive, an instance or a model.
-template <bool COUNT>
-MRT_DEV void trav_prim(const DevScene& S, const uint4* slots, Trav& t, LocalCounters& lc) {
+// The current record is a primitive, an instance or a model. ALPHA=false is
+// the specialisation for scenes without alpha-tested triangles (the alpha
+// test's registers would otherwise cost occupancy everywhere).
+template <bool COUNT, bool ALPHA>
+MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
+  const DevScene& S = in.S;
   const uint4 s0 = t.s0, s1 = t.s1;
   const uint32_t kind = s1.w;
   if (kind == KIND_TRI) {
     if (COUNT) lc.triangle_tests++;
-    const uint4 s2 = slots[MRT_IDX(S, t.i + 2, S.n_slots, 7)];
+    const uint4 s2 = in.slots[MRT_IDX(S, t.i + 2, S.n_slots, 7)];
     V3 a{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, ab{u2f(s0.w), u2f(s1.x), u2f(s1.y)}, ac{u2f(s2.x), u2f(s2.y), u2f(s2.z)};
     float th;
-    if (tri_hit(a, ab, ac, t.r.o, t.r.d, t.tmin, t.best, th)) {
-      if (!(s2.w & TRI_FLAG_ALPHA) || tri_alpha_pass(S, s1.z, t.r.o, t.r.d, th, lc)) {
+    if (tri_hit(a, ab, ac, t.r.o, t.r.d, in.tmin, t.best, th)) {
+      if (!ALPHA || !(s2.w & TRI_FLAG_ALPHA) || tri_alpha_pass(S, s1.z, t.r.o, t.r.d, th, lc)) {
         t.best = th;
-        t.h = Hit{th, make_ref(MRT_REF_TRIANGLE, s1.z), t.container};
+        t.prim = make_ref(MRT_REF_TRIANGLE, s1.z);
+        t.hit_ret = t.ret;
       }
     }
     t.i += 3;
   } else if (kind == KIND_SPHERE) {
     if (COUNT) lc.sphere_tests++;
     float th;
-    if (sphere_hit(V3{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, u2f(s0.w), t.r.o, t.r.d, t.r.a, t.tmin, t.best, th)) {
+    if (sphere_hit(V3{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, u2f(s0.w), t.r.o, t.r.d, t.r.a, in.tmin, t.best, th)) {
       t.best = th;
-      t.h = Hit{th, make_ref(MRT_REF_SPHERE, s1.x), t.container};
+      t.prim = make_ref(MRT_REF_SPHERE, s1.x);
+      t.hit_ret = t.ret;
     }
     t.i += 2;
   } else if (kind == KIND_INST) {
     if (COUNT) lc.instance_entries++;
     V3 c0, c1, c2, c3;
     load_m12(S.inst_inv + (size_t)MRT_IDX(S, s0.x, S.n_inst, 8) * 12, c0, c1, c2, c3);
-    t.r = make_tray(xform(c0, c1, c2, c3, t.world.o, 1.0f), xform(c0, c1, c2, c3, t.world.d, 0.0f), S.fast_ok);
-    t.container = make_ref(MRT_REF_INSTANCE, s0.x);
-    t.ret = t.i + 2;
+    // entered from the world region: t.r is the world ray here
+    t.r = make_tray(xform(c0, c1, c2, c3, t.r.o, 1.0f), xform(c0, c1, c2, c3, t.r.d, 0.0f), S.fast_ok);
+    t.ret = (t.i + 2) | kRetInstance;
     t.i = s0.y;
     t.end = s0.z;
   } else {  // KIND_MODEL
     if (COUNT) lc.model_entries++;
-    t.container = make_ref(MRT_REF_MODEL, s0.x);
     t.ret = t.i + 2;
     t.i = s0.y;
     t.end = s0.z;
   }
-  trav_fetch(S, slots, t);
+  trav_fetch(in, t);
 }
 
+// Whole traversal of pool ray `ray` (one ray per thread).
 template <bool COUNT>
-MRT_DEV Hit closest_hit(const DevScene& S, V3 o, V3 d, float tmin, float tmax, LocalCounters& lc) {
+MRT_DEV Hit closest_hit(const TravIn& in, uint32_t ray, float tmax, LocalCounters& lc) {
   Trav t;
-  const uint4* slots = reinterpret_cast<const uint4*>(S.slots);
-  trav_init(S, slots, t, o, d, tmin, tmax);
+  trav_init(in, t, ray, tmax);
   while (!t.done) {
     if (trav_at_box(t))
-      trav_box<COUNT>(S, slots, t, lc);
+      trav_box<COUNT>(in, t, lc);
     else
-      trav_prim<COUNT>(S, slots, t, lc);
+      trav_prim<COUNT, true>(in, t, lc);
   }
-  return t.h;
+  return trav_hit(in, t);
 }
 
 // Hit record of the closest hit, computed the way the reference's winning

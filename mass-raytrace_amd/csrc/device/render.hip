@@ -150,18 +150,25 @@ __global__ __launch_bounds__(kBlock) void k_generate(DevCamera cam, RenderParams
 // ray of the wave's chunk as soon as enough lanes are idle, so the SIMD keeps
 // issuing for busy lanes instead of waiting for the wave's slowest ray.
 constexpr float kTmin = 0.001f;          // World::intersect(ray, 0.001, INFINITY) (main.rs trace)
-constexpr uint32_t kTraceChunk = 256;  // rays per atomic grab
-constexpr uint32_t kRefill = 16;       // refill once this many lanes idle
-constexpr uint32_t kPrimBatch = 8;     // run the primitive branch once this many lanes wait at one
+// Scheduling knobs of the persistent loop (kernel arguments so that they can
+// be tuned without a rebuild: MRT_TRACE_REFILL / _PRIM_BATCH / _CHUNK).
+constexpr uint64_t kResultsMax = 256ull << 20;  // samples per results slab (4 GiB)
+
+struct TraceTune {
+  uint32_t chunk = 128;     // rays per atomic grab
+  uint32_t refill = 16;     // refill once this many lanes idle
+  uint32_t prim_batch = 8;  // run the primitive branch once this many lanes wait at one
+};
 
 // LDS=true: the whole record stream is first copied into the workgroup's LDS
 // (scenes up to kTraceLdsMaxBytes, e.g. SphereGrid's ~31 KB), so every
 // traversal step reads LDS instead of L1/L2.
 constexpr size_t kTraceLdsMaxBytes = 64 * 1024;
+constexpr uint32_t kIdle = 0xFFFFFFFFu;  // Trav.ray of a lane without a ray
 
-template <bool COUNT, bool LDS>
+template <bool COUNT, bool LDS, bool ALPHA>
 __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
-                                                  DevCounters* cnt, float tmin, float tmax) {
+                                                  DevCounters* cnt, float tmin, float tmax, TraceTune tune) {
   extern __shared__ uint4 lds_slots[];
   const uint32_t n = ctrl->active[cur];
   if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = 0;
@@ -171,50 +178,47 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
     for (uint32_t k = threadIdx.x; k < S.n_slots; k += kBlock) lds_slots[k] = gslots[k];
     __syncthreads();
   }
-  const uint4* slots = LDS ? lds_slots : gslots;
+  const TravIn tin{S, LDS ? lds_slots : gslots, in.ro, in.rd, tmin};
   LocalCounters lc;
   uint32_t seg = 0, nh = 0;
   uint32_t pool = 0, pool_end = 0;  // wave-uniform chunk [pool, pool_end)
   bool drained = false;             // wave-uniform: the counter passed n
-  uint32_t ray = 0xFFFFFFFFu;
   Trav t{};  // fully initialised: idle lanes must not carry undefined state
   t.done = true;
+  t.ray = kIdle;
   for (;;) {
-    const unsigned long long idle = __ballot(ray == 0xFFFFFFFFu);
+    const unsigned long long idle = __ballot(t.ray == kIdle);
     const uint32_t n_idle = (uint32_t)__popcll(idle);
-    if (n_idle >= kRefill || n_idle == 64) {
+    if (n_idle >= tune.refill || n_idle == 64) {
       if (pool == pool_end && !drained) {  // grab the next chunk (wave-uniform)
         uint32_t b = 0;
-        if (lane_id() == 0) b = atomicAdd(&ctrl->trace_next, kTraceChunk);
+        if (lane_id() == 0) b = atomicAdd(&ctrl->trace_next, tune.chunk);
         b = __shfl(b, 0, 64);
         pool = b < n ? b : n;
-        pool_end = b + kTraceChunk < n ? b + kTraceChunk : n;
-        drained = b + kTraceChunk >= n;
+        pool_end = b + tune.chunk < n ? b + tune.chunk : n;
+        drained = b + tune.chunk >= n;
       }
       const uint32_t avail = pool_end - pool;
-      if (ray == 0xFFFFFFFFu) {
+      if (t.ray == kIdle) {
         const uint32_t r = lane_rank(idle);
-        if (r < avail) {
-          ray = MRT_IDX(S, pool + r, n, 20);
-          const float4 o4 = in.ro[ray], d4 = in.rd[ray];
-          trav_init(S, slots, t, V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, tmin, tmax);
-        }
+        if (r < avail) trav_init(tin, t, MRT_IDX(S, pool + r, n, 20), tmax);
       }
       pool += n_idle < avail ? n_idle : avail;
-      if (__ballot(ray != 0xFFFFFFFFu) == 0) break;  // chunk source exhausted
+      if (__ballot(t.ray != kIdle) == 0) break;  // chunk source exhausted
     }
     const bool busy = !t.done;  // idle lanes hold a done Trav
     const bool at_box = busy && trav_at_box(t);
     const unsigned long long box_mask = __ballot(at_box);
     const unsigned long long prim_mask = __ballot(busy && !at_box);
-    if (at_box) trav_box<COUNT>(S, slots, t, lc);
+    if (at_box) trav_box<COUNT>(tin, t, lc);
     // primitives wait until enough lanes are at one (or no lane is at a box)
-    if ((__popcll(prim_mask) >= kPrimBatch || box_mask == 0) && busy && !at_box) trav_prim<COUNT>(S, slots, t, lc);
-    if (ray != 0xFFFFFFFFu && t.done) {
-      hits[ray] = make_uint4(__float_as_uint(t.h.t), t.h.prim, t.h.container, 0u);
+    if ((__popcll(prim_mask) >= tune.prim_batch || box_mask == 0) && busy && !at_box) trav_prim<COUNT, ALPHA>(tin, t, lc);
+    if (t.ray != kIdle && t.done) {
+      const Hit h = trav_hit(tin, t);
+      hits[t.ray] = make_uint4(__float_as_uint(h.t), h.prim, h.container, 0u);
       seg += 1;
-      nh += t.h.prim != kRefNone;
-      ray = 0xFFFFFFFFu;
+      nh += t.prim != kRefNone;
+      t.ray = kIdle;
     }
   }
   if (COUNT) flush_counters(cnt, lc, seg, nh, 0, 0);
@@ -228,9 +232,9 @@ __global__ __launch_bounds__(kBlock) void k_trace_simple(DevScene S, PathBufs in
   if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = 0;
   LocalCounters lc;
   uint32_t seg = 0, nh = 0;
+  const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), in.ro, in.rd, kTmin};
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    const float4 o4 = in.ro[i], d4 = in.rd[i];
-    Hit h = closest_hit<true>(S, V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, 0.001f, INFINITY, lc);
+    Hit h = closest_hit<true>(tin, i, INFINITY, lc);
     hits[i] = make_uint4(__float_as_uint(h.t), h.prim, h.container, 0u);
     seg += 1;
     nh += h.prim != kRefNone;
@@ -433,6 +437,76 @@ __global__ __launch_bounds__(kBlock) void k_selftest_division(unsigned long long
   if (lane_id() == 0 && bad) atomicAdd(mismatches, bad);
 }
 
+
+// box_hit_any (early decision + exact fallback) against box_hit_exact on
+// rays in the fast domain and boxes whose faces pass within a few ulps of a
+// point of the ray (entry/exit ties), flat boxes, and t_max near the faces.
+__global__ __launch_bounds__(kBlock) void k_selftest_slab(unsigned long long n, unsigned long long seed,
+                                                          unsigned long long* out) {
+  unsigned long long bad = 0, ties = 0;
+  const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
+  for (unsigned long long i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    uint64_t x = seed ^ (i * 0xD1B54A32D192ED03ull);
+    auto rnd = [&]() { return splitmix64_next(x); };
+    auto coord = [&](uint64_t r) {  // {0} U [2^-40, 2^27], random sign
+      uint32_t e = 87u + (uint32_t)((r >> 32) % 68u);
+      float v = __uint_as_float(((uint32_t)r & 0x807FFFFFu) | (e << 23));
+      return ((r >> 60) & 15u) == 0 ? 0.0f : v;
+    };
+    auto dir = [&](uint64_t r) {  // |d| in [2^-20, 2^19]
+      uint32_t e = 107u + (uint32_t)((r >> 32) % 40u);
+      return __uint_as_float(((uint32_t)r & 0x807FFFFFu) | (e << 23));
+    };
+    auto nudge = [](float v, int k) { return __uint_as_float(__float_as_uint(v) + k); };
+    V3 o{coord(rnd()), coord(rnd()), coord(rnd())};
+    const uint64_t sc = rnd();
+    if (sc & 1) {  // scene-like magnitudes
+      o = V3{(float)((int)(sc >> 8 & 255) - 128) * 0.37f, (float)((int)(sc >> 16 & 255) - 128) * 0.11f,
+             (float)((int)(sc >> 24 & 255) - 128) * 0.23f};
+    }
+    V3 d{dir(rnd()), dir(rnd()), dir(rnd())};
+    const float t = __uint_as_float((uint32_t)(((uint64_t)117u + (rnd() % 20u)) << 23) | ((uint32_t)rnd() & 0x7FFFFFu));
+    const V3 p = o + d * t;
+    float mn[3], mx[3];
+    const float pv[3] = {p.x, p.y, p.z};
+    for (int k = 0; k < 3; ++k) {
+      const uint64_t r = rnd();
+      const int a = (int)(r & 7), b = (int)((r >> 3) & 7);
+      const float lo = (r >> 6 & 3) == 0 ? pv[k] - fabsf(pv[k]) * 0.25f - 0.5f : nudge(pv[k], -a);
+      const float hi = (r >> 8 & 3) == 0 ? pv[k] + fabsf(pv[k]) * 0.25f + 0.5f : nudge(pv[k], b);
+      mn[k] = fminf(lo, hi);
+      mx[k] = fmaxf(lo, hi);
+      if ((r >> 10 & 7) == 0) mx[k] = mn[k];  // flat box
+    }
+    bool ok = true;
+    for (int k = 0; k < 3; ++k) ok = ok && coord_ok(mn[k]) && coord_ok(mx[k]);
+    if (!ok) continue;
+    const TRay ray = make_tray(o, d, true);
+    if (!ray.fast) continue;
+    const uint64_t rt = rnd();
+    const float tmin = (rt & 3) == 0 ? nudge(t, -(int)(rt >> 2 & 3)) : 0.001f;
+    const float tmax = (rt >> 4 & 3) == 0 ? INFINITY : ((rt >> 4 & 3) == 1 ? nudge(t, (int)(rt >> 6 & 7) - 3) : t * 2.0f);
+    const V3 bmn{mn[0], mn[1], mn[2]}, bmx{mx[0], mx[1], mx[2]};
+    const bool e = box_hit_exact(bmn, bmx, ray, tmin, tmax);
+    const bool f = box_hit_any(bmn, bmx, ray, tmin, tmax);
+    bad += e != f;
+    // count how often the exact fallback had to decide
+    V3 na = bmn - ray.o, nb = bmx - ray.o;
+    const float ax = na.x * ray.yx, ay = na.y * ray.yy, az = na.z * ray.yz;
+    const float bx = nb.x * ray.yx, by = nb.y * ray.yy, bz = nb.z * ray.yz;
+    const float t0 = vmax3(vmin1(ax, bx), vmin1(ay, by), vmax1(vmin1(az, bz), tmin));
+    const float t1 = vmin3(vmax1(ax, bx), vmax1(ay, by), vmin1(vmax1(az, bz), tmax));
+    const float m = (fabsf(t0) + fabsf(t1)) * 0x1p-19f;
+    ties += !(t1 - t0 > m) && !(t0 - t1 > m);
+  }
+  bad = (unsigned long long)wave_sum((uint32_t)bad);
+  ties = (unsigned long long)wave_sum((uint32_t)ties);
+  if (lane_id() == 0 && (bad || ties)) {
+    atomicAdd(out, bad);
+    atomicAdd(out + 1, ties);
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -459,7 +533,16 @@ struct mrt_ctx {
   uint32_t* dbg = nullptr;  // MRT_DEBUG_BOUNDS record (4 words)
   Ctrl* h_status = nullptr;  // pinned, 2 slots
   hipEvent_t ev[2]{};
-  uint32_t trace_grid = 1024;  // persistent k_trace workgroups (set from the CU count)
+  uint32_t trace_grid = 1024;  // persistent k_trace workgroups of the current scene's variant
+  uint32_t trace_grid_alpha = 1024, trace_grid_noalpha = 1024;  // (set from the CU count and occupancy)
+  bool scene_alpha = true;  // the scene has alpha-tested triangles
+  TraceTune tune;
+  // Live paths per iteration (MRT_POOL_PATHS overrides). Large on purpose:
+  // every k_trace launch ends with a tail of long rays on few lanes, so the
+  // more rays a launch carries the smaller that tail's share (measured on
+  // SphereGrid 1080p: 2M paths 186, 16M 377, 64M 434 Msamples/s). 64M paths
+  // hold 11 GiB of HBM (176 B each).
+  size_t pool_paths = (size_t)64 << 20;
   int cus = 1;
   bool trace_lds = false;          // record stream staged in LDS (set per scene)
   uint32_t trace_grid_lds = 1024;  // workgroups of the LDS variant
@@ -515,25 +598,33 @@ size_t align_up(size_t x) {
   return (x + 255) & ~(size_t)255;
 }
 
-// The persistent closest-hit kernel over pool buffer `in` (LDS variant when
-// the scene's record stream fits).
+// The persistent closest-hit kernel over pool buffer `in`, specialised on
+// the scene (record stream in LDS when it fits; alpha test compiled in only
+// when the scene has alpha-textured triangles).
+template <bool LDS, bool ALPHA>
+void launch_trace_v(mrt_ctx* c, hipStream_t st, const PathBufs& in, uint32_t cur, bool count, float tmin,
+                    float tmax) {
+  const size_t smem = LDS ? (size_t)c->S.n_slots * 16 : 0;
+  const dim3 grid(LDS ? c->trace_grid_lds : c->trace_grid);
+  if (count)
+    hipLaunchKernelGGL((k_trace<true, LDS, ALPHA>), grid, dim3(kBlock), smem, st, c->S, in, c->hits, c->ctrl, cur,
+                       c->d_cnt, tmin, tmax, c->tune);
+  else
+    hipLaunchKernelGGL((k_trace<false, LDS, ALPHA>), grid, dim3(kBlock), smem, st, c->S, in, c->hits, c->ctrl, cur,
+                       c->d_cnt, tmin, tmax, c->tune);
+}
+
 void launch_trace(mrt_ctx* c, hipStream_t st, const PathBufs& in, uint32_t cur, bool count, float tmin, float tmax) {
-  const DevScene& S = c->S;
   if (c->trace_lds) {
-    const size_t smem = (size_t)S.n_slots * 16;
-    if (count)
-      hipLaunchKernelGGL((k_trace<true, true>), dim3(c->trace_grid_lds), dim3(kBlock), smem, st, S, in, c->hits,
-                         c->ctrl, cur, c->d_cnt, tmin, tmax);
+    if (c->scene_alpha)
+      launch_trace_v<true, true>(c, st, in, cur, count, tmin, tmax);
     else
-      hipLaunchKernelGGL((k_trace<false, true>), dim3(c->trace_grid_lds), dim3(kBlock), smem, st, S, in, c->hits,
-                         c->ctrl, cur, c->d_cnt, tmin, tmax);
+      launch_trace_v<true, false>(c, st, in, cur, count, tmin, tmax);
   } else {
-    if (count)
-      hipLaunchKernelGGL((k_trace<true, false>), dim3(c->trace_grid), dim3(kBlock), 0, st, S, in, c->hits, c->ctrl,
-                         cur, c->d_cnt, tmin, tmax);
+    if (c->scene_alpha)
+      launch_trace_v<false, true>(c, st, in, cur, count, tmin, tmax);
     else
-      hipLaunchKernelGGL((k_trace<false, false>), dim3(c->trace_grid), dim3(kBlock), 0, st, S, in, c->hits, c->ctrl,
-                         cur, c->d_cnt, tmin, tmax);
+      launch_trace_v<false, false>(c, st, in, cur, count, tmin, tmax);
   }
   HIP_CHECK(hipGetLastError());
 }
@@ -609,9 +700,9 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
   const uint32_t n_pix = pl.second;
   if (n_pix == 0) return;
   const bool count = (a->flags & MRT_RENDER_COUNTERS) != 0;
-  // results slab <= 64M samples (1 GiB); pool <= 2M paths
-  uint32_t spp_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(a->spp_count, (64ull << 20) / n_pix));
-  const size_t pool = std::min<size_t>((size_t)n_pix * spp_chunk, (size_t)2 << 20);
+  // results slab <= kResultsMax samples (16 B each); pool <= c->pool_paths
+  uint32_t spp_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(a->spp_count, kResultsMax / n_pix));
+  const size_t pool = std::min<size_t>((size_t)n_pix * spp_chunk, c->pool_paths);
   ensure_pool(c, pool);
   ensure_results(c, (size_t)n_pix * spp_chunk);
   for (uint32_t done = 0; done < a->spp_count; done += spp_chunk) {
@@ -756,11 +847,19 @@ int mrt_create(int device, mrt_ctx** out) {
     // persistent k_trace: as many resident workgroups as the register budget
     // allows on every CU (MRT_TRACE_WGS_PER_CU overrides, for tuning)
     int per_cu = 0;
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false>, kBlock, 0));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false, true>, kBlock, 0));
     if (const char* e = getenv("MRT_TRACE_WGS_PER_CU")) per_cu = atoi(e);
     c->cus = std::max(1, cus);
-    c->trace_grid = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
-    for (auto f : {(const void*)k_trace<false, true>, (const void*)k_trace<true, true>})
+    if (const char* e = getenv("MRT_TRACE_REFILL")) c->tune.refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
+    if (const char* e = getenv("MRT_TRACE_PRIM_BATCH")) c->tune.prim_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
+    if (const char* e = getenv("MRT_TRACE_CHUNK")) c->tune.chunk = (uint32_t)std::max(64, atoi(e));
+    if (const char* e = getenv("MRT_POOL_PATHS")) c->pool_paths = (size_t)std::max(1 << 16, std::min(1 << 28, atoi(e)));
+    c->trace_grid_alpha = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false, false>, kBlock, 0));
+    if (const char* e = getenv("MRT_TRACE_WGS_PER_CU")) per_cu = atoi(e);
+    c->trace_grid_noalpha = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
+    for (auto f : {(const void*)k_trace<false, true, false>, (const void*)k_trace<true, true, false>,
+                   (const void*)k_trace<false, true, true>, (const void*)k_trace<true, true, true>})
       HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTraceLdsMaxBytes));
   });
   if (rc != MRT_OK) {
@@ -866,9 +965,14 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     const size_t lds_bytes = (size_t)S.n_slots * 16;
     const char* no_lds = getenv("MRT_TRACE_LDS");
     c->trace_lds = lds_bytes <= kTraceLdsMaxBytes && !(no_lds && no_lds[0] == '0');
+    c->scene_alpha = hs.has_alpha;
+    c->trace_grid = c->scene_alpha ? c->trace_grid_alpha : c->trace_grid_noalpha;
     if (c->trace_lds) {
       int per_cu = 0;
-      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, true>, kBlock, lds_bytes));
+      if (c->scene_alpha)
+        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, true, true>, kBlock, lds_bytes));
+      else
+        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, true, false>, kBlock, lds_bytes));
       c->trace_grid_lds = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
     }
     c->has_scene = true;
@@ -1010,6 +1114,24 @@ int mrt_selftest_division(mrt_ctx* c, uint64_t n, uint64_t seed, uint64_t* misma
     HIP_CHECK(hipStreamSynchronize(c->stream));
     HIP_CHECK(hipFree(d));
     *mismatches = h;
+  });
+}
+
+int mrt_selftest_slab(mrt_ctx* c, uint64_t n, uint64_t seed, uint64_t* mismatches, uint64_t* near_ties) {
+  return guarded(c, [&] {
+    if (!mismatches || !near_ties) throw ApiError{MRT_ERR_INVALID, "null output"};
+    unsigned long long* d = nullptr;
+    HIP_CHECK(hipMalloc(&d, 16));
+    HIP_CHECK(hipMemsetAsync(d, 0, 16, c->stream));
+    hipLaunchKernelGGL(k_selftest_slab, dim3(4096), dim3(kBlock), 0, c->stream, (unsigned long long)n,
+                       (unsigned long long)seed, d);
+    HIP_CHECK(hipGetLastError());
+    unsigned long long h[2] = {0, 0};
+    HIP_CHECK(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    HIP_CHECK(hipFree(d));
+    *mismatches = h[0];
+    *near_ties = h[1];
   });
 }
 

@@ -48,7 +48,10 @@ struct Emitter {
         for (int k = 0; k < 3; ++k) ab[k] = t.b[k] - t.a[k], ac[k] = t.c[k] - t.a[k];
         uint32_t flags = 0;
         if (t.flags & MRT_TRI_HAS_UV) flags |= TRI_FLAG_UV;
-        if (needs_alpha(t)) flags |= TRI_FLAG_ALPHA;
+        if (needs_alpha(t)) {
+          flags |= TRI_FLAG_ALPHA;
+          s.has_alpha = true;
+        }
         push_slot(fbits(t.a[0]), fbits(t.a[1]), fbits(t.a[2]), fbits(ab[0]));
         push_slot(fbits(ab[1]), fbits(ab[2]), idx, KIND_TRI);
         push_slot(fbits(ac[0]), fbits(ac[1]), fbits(ac[2]), flags);
@@ -262,6 +265,7 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
     s.slots[4 * p.first + 1] = it->second.first;
     s.slots[4 * p.first + 2] = it->second.second;
   }
+  if (s.slots.size() / 4 >= 0x80000000ull) return (err = "scene too large (record stream >= 2^31 slots)", false);
   return true;
 }
 

@@ -20,6 +20,7 @@ struct HostScene {
   std::vector<GpuTexture> textures;
   std::vector<uint32_t> texels;
   uint32_t fast_ok = 1;
+  bool has_alpha = false;  // some triangle carries TRI_FLAG_ALPHA
   uint32_t bg_kind = 0, bg_texture = 0, bg_surf_kind = 0;
   float bg_color[4] = {0, 0, 0, 0};
   // statistics

@@ -150,7 +150,7 @@ EXPORTED_SYMBOLS = [
     "mrt_create", "mrt_destroy", "mrt_last_error", "mrt_global_last_error", "mrt_abi_version",
     "mrt_upload_scene", "mrt_set_camera", "mrt_render", "mrt_render_device", "mrt_trace_rays",
     "mrt_get_counters", "mrt_reset_counters", "mrt_scene_device_bytes", "mrt_get_kernel_stats",
-    "mrt_reset_kernel_stats", "mrt_selftest_division", "mrt_debug_status", "mrt_debug_build",
+    "mrt_reset_kernel_stats", "mrt_selftest_division", "mrt_selftest_slab", "mrt_debug_status", "mrt_debug_build",
     "mrt_builder_new", "mrt_builder_free", "mrt_builder_builtin", "mrt_builder_rand_f32", "mrt_builder_solid",
     "mrt_builder_texture_png", "mrt_builder_texture_rgba", "mrt_builder_material", "mrt_builder_background",
     "mrt_builder_add_sphere", "mrt_builder_add_triangle", "mrt_builder_model", "mrt_builder_model_from_ply",
@@ -188,6 +188,7 @@ def lib() -> C.CDLL:
         "mrt_get_kernel_stats": (I, [P, C.POINTER(MrtKernelStats)]),
         "mrt_reset_kernel_stats": (I, [P]),
         "mrt_selftest_division": (I, [P, U64, U64, C.POINTER(C.c_uint64)]),
+        "mrt_selftest_slab": (I, [P, U64, U64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "mrt_debug_status": (I, [P, C.POINTER(C.c_uint32)]),
         "mrt_debug_build": (I, []),
         "mrt_scene_device_bytes": (I, [P, C.POINTER(C.c_uint64)]),
@@ -451,6 +452,12 @@ class Context:
         m = C.c_uint64()
         self._check(lib().mrt_selftest_division(self.h, n, seed, C.byref(m)))
         return int(m.value)
+
+    def selftest_slab(self, n: int, seed: int = 1):
+        """(mismatches, near_ties) of the early slab decision vs the exact test."""
+        m, t = C.c_uint64(), C.c_uint64()
+        self._check(lib().mrt_selftest_slab(self.h, n, seed, C.byref(m), C.byref(t)))
+        return int(m.value), int(t.value)
 
     def debug_status(self):
         out = (C.c_uint32 * 4)()

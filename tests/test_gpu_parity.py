@@ -306,3 +306,13 @@ def test_device_division_is_correctly_rounded(ctx):
     corrections (path.h div_cr); it must equal a/b bit for bit."""
     assert ctx.selftest_division(1 << 30, seed=1) == 0
     assert ctx.selftest_division(1 << 28, seed=12345) == 0
+
+
+def test_slab_early_decision_matches_exact(ctx):
+    """box_hit_any decides most slab tests from approximate quotients with an
+    error margin (path.h); on grazing rays, flat boxes and t_max at a face it
+    must agree with the exact (correctly rounded) slab test every time."""
+    for seed in (1, 99):
+        bad, ties = ctx.selftest_slab(1 << 26, seed=seed)
+        assert bad == 0
+        assert ties > 100_000  # the near-tie fallback is exercised

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Tuning session: GPU parity subset, then bench variants (env A/B) — each step time-limited.
 mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -q -x -k "not mesh" > gpurun_out/quick_tests.log 2>&1 || { echo tests failed; tail -30 gpurun_out/quick_tests.log; exit 1; }
+timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -q -x -k "not mesh_scene" > gpurun_out/quick_tests.log 2>&1 || { echo tests failed; tail -30 gpurun_out/quick_tests.log; exit 1; }
 tail -1 gpurun_out/quick_tests.log
 i=0
 for v in "${@:-X=1}"; do

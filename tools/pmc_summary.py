@@ -26,7 +26,7 @@ def rows(pattern):
 def short(name):
     for k in ("k_trace_rays", "k_trace", "k_shade", "k_generate", "k_accumulate"):
         if k in name:
-            return k + ("[counting]" if "<true>" in name else "")
+            return k + ("[counting]" if f"{k}<true" in name else "")
     return name[:40]
 
 
