@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--fused", action="store_true", help="one persistent k_render instead of the k_trace/k_shade loop")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--pmc-json", default=None, help="PMC summary (default profiles/pmc_<scene>.json)")
     return ap.parse_args()
@@ -131,7 +132,8 @@ def main():
 
     def step(counters=False, timing=False):
         def render_into(rgb, bounces, s0, n):
-            args = ctx.args(W, H, s0, n, a.seed, a.max_depth, rank, world, counters=counters, time_kernels=timing)
+            args = ctx.args(W, H, s0, n, a.seed, a.max_depth, rank, world, counters=counters, time_kernels=timing,
+                            flags=massrt.RENDER_FUSED if a.fused else 0)
             ctx.render_device(args, rgb.data_ptr(), bounces.data_ptr(), stream)
 
         frame.step(render_into, spp)  # renders this rank's tiles, then one reduce onto rank 0

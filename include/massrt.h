@@ -188,6 +188,8 @@ typedef struct {
 #define MRT_RENDER_COUNTERS 1u     /* collect traversal counters (slower) */
 #define MRT_RENDER_TIME_KERNELS 2u /* time every k_trace/k_shade launch with HIP events */
 #define MRT_RENDER_SIMPLE_TRACE 4u /* debug: one-ray-per-thread closest hit instead of the persistent k_trace */
+#define MRT_RENDER_FUSED 8u        /* one persistent k_render (trace + shade per lane) instead of the
+                                      k_trace/k_shade wavefront loop; same results, slower at 108 VGPRs */
 
 /* Closest hit of one ray (parity entry point). */
 typedef struct {

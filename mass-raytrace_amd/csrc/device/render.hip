@@ -156,8 +156,9 @@ constexpr uint64_t kResultsMax = 256ull << 20;  // samples per results slab (4 G
 
 struct TraceTune {
   uint32_t chunk = 128;     // rays per atomic grab
-  uint32_t refill = 16;     // refill once this many lanes idle
-  uint32_t prim_batch = 8;  // run the primitive branch once this many lanes wait at one
+  uint32_t refill = 32;      // refill once this many lanes idle
+  uint32_t prim_batch = 16;  // run the primitive branch once this many lanes wait at one
+  uint32_t shade_batch = 16; // k_render: shade once this many lanes finished a segment
 };
 
 // LDS=true: the whole record stream is first copied into the workgroup's LDS
@@ -242,6 +243,29 @@ __global__ __launch_bounds__(kBlock) void k_trace_simple(DevScene S, PathBufs in
   flush_counters(cnt, lc, seg, nh, 0, 0);
 }
 
+// One level of main.rs trace() after World::intersect returned `h` for the
+// ray (o, d): adds T * emitted (hit) or T * background (miss) to L; on a
+// scatter that continues (and depth left) moves (o, d) to the scattered ray,
+// multiplies T by the attenuation and returns true.
+MRT_DEV bool shade_step(const DevScene& S, uint32_t max_depth, const Hit& h, V3& o, V3& d, V3& T, V3& L, uint32_t& k,
+                        PathRng& rng, LocalCounters& lc, uint32_t& nbounce) {
+  if (h.prim == kRefNone) {
+    L = L + T * background(S, d, lc);
+    return false;
+  }
+  Surf s = resolve_hit(S, o, d, h);
+  V3 emitted, atten, nd;
+  bool cont = scatter(S, s, d, rng, emitted, atten, nd, lc);
+  L = L + T * emitted;
+  if (!cont) return false;
+  T = T * atten;
+  k += 1;
+  nbounce += 1;
+  o = s.point;
+  d = nd;
+  return k < max_depth;  // trace(depth 0) returns (0, 0)
+}
+
 template <bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, DevCamera cam, RenderParams rp, PathBufs in,
                                                   PathBufs out, const uint4* hits, Ctrl* ctrl, uint32_t cur,
@@ -268,23 +292,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, DevCamera cam, Ren
     uint32_t g = __float_as_uint(ro.w), k = __float_as_uint(rd.w);
     PathRng rng{(unsigned long long)rs.x | ((unsigned long long)rs.y << 32),
                 (unsigned long long)rs.z | ((unsigned long long)rs.w << 32)};
-    bool cont = false;
-    if (h.prim != kRefNone) {
-      Surf s = resolve_hit(S, o, d, h);
-      V3 emitted, atten, nd;
-      cont = scatter(S, s, d, rng, emitted, atten, nd, lc);
-      L = L + T * emitted;
-      if (cont) {
-        T = T * atten;
-        k += 1;
-        nbounce = 1;
-        o = s.point;
-        d = nd;
-        if (k >= rp.max_depth) cont = false;  // trace(depth 0) returns (0, 0)
-      }
-    } else {
-      L = L + T * background(S, d, lc);
-    }
+    const bool cont = shade_step(S, rp.max_depth, h, o, d, T, L, k, rng, lc, nbounce);
     if (cont) {
       alive = true;
       ro = make_float4(o.x, o.y, o.z, __uint_as_float(g));
@@ -326,6 +334,96 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, DevCamera cam, Ren
     out.rng[pos] = rs;
   }
   if (COUNT) flush_counters(cnt, lc, 0, 0, nsample, nbounce);
+}
+
+// The whole path loop in one persistent kernel: every lane owns a path
+// (work item g = sample*n_pix + pixel), steps its closest-hit traversal like
+// k_trace, and when a segment ends shades it in place (shade_step) and
+// continues with the scattered ray — no pool buffers, no per-bounce launch
+// and no per-launch tail. Finished paths write results[g] (accumulated in
+// sample order by k_accumulate, so the image is independent of scheduling);
+// idle lanes take new work items from ctrl->next_work. slot_ro/slot_rd hold
+// each lane's current world ray (re-read when leaving an instance and when
+// shading, instead of keeping it in registers).
+template <bool COUNT, bool LDS, bool ALPHA>
+__global__ __launch_bounds__(kBlock) void k_render(DevScene S, DevCamera cam, RenderParams rp, float4* slot_ro,
+                                                   float4* slot_rd, Ctrl* ctrl, float4* results, DevCounters* cnt,
+                                                   TraceTune tune) {
+  extern __shared__ uint4 lds_slots[];
+  const uint4* gslots = reinterpret_cast<const uint4*>(S.slots);
+  if (LDS) {
+    for (uint32_t q = threadIdx.x; q < S.n_slots; q += kBlock) lds_slots[q] = gslots[q];
+    __syncthreads();
+  }
+  const uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
+  const TravIn tin{S, LDS ? lds_slots : gslots, slot_ro, slot_rd, kTmin};
+  LocalCounters lc;
+  uint32_t seg = 0, nh = 0, nsamples = 0, nbounces = 0;
+  Trav t{};
+  t.done = true;
+  t.ray = slot;
+  uint32_t g = kIdle, k = 0;
+  V3 T{0, 0, 0}, L{0, 0, 0};
+  PathRng rng{0, 0};
+  bool drained = false;  // wave-uniform: the work counter passed G
+  for (;;) {
+    const unsigned long long idle = __ballot(g == kIdle);
+    const uint32_t n_idle = (uint32_t)__popcll(idle);
+    if (!drained && (n_idle >= tune.refill || n_idle == 64)) {
+      uint32_t b = 0;
+      if (lane_id() == 0) b = atomicAdd(&ctrl->next_work, n_idle);
+      b = __shfl(b, 0, 64);
+      drained = b + n_idle >= rp.G;
+      if (g == kIdle) {
+        const uint32_t w = b + lane_rank(idle);
+        if (w < rp.G) {
+          float4 ro, rd;
+          uint4 rs;
+          gen_work(cam, rp, w, ro, rd, rs);
+          g = w;
+          k = 0;
+          T = V3{1.0f, 1.0f, 1.0f};
+          L = V3{0.0f, 0.0f, 0.0f};
+          rng = PathRng{(unsigned long long)rs.x | ((unsigned long long)rs.y << 32),
+                        (unsigned long long)rs.z | ((unsigned long long)rs.w << 32)};
+          slot_ro[slot] = ro;
+          slot_rd[slot] = rd;
+          trav_init(tin, t, slot, INFINITY);
+        }
+      }
+    }
+    if (drained && __ballot(g != kIdle) == 0) break;
+    // one traversal step (as k_trace)
+    const bool busy = g != kIdle && !t.done;
+    const bool at_box = busy && trav_at_box(t);
+    const unsigned long long box_mask = __ballot(at_box);
+    const unsigned long long prim_mask = __ballot(busy && !at_box);
+    if (at_box) trav_box<COUNT>(tin, t, lc);
+    if ((__popcll(prim_mask) >= tune.prim_batch || box_mask == 0) && busy && !at_box)
+      trav_prim<COUNT, ALPHA>(tin, t, lc);
+    // shade finished segments once enough lanes wait (or nothing else runs)
+    const bool ready = g != kIdle && t.done;
+    const unsigned long long ready_mask = __ballot(ready);
+    if (ready_mask != 0 && ((uint32_t)__popcll(ready_mask) >= tune.shade_batch || (box_mask | prim_mask) == 0)) {
+      if (ready) {
+        const Hit h = trav_hit(tin, t);
+        seg += 1;
+        nh += h.prim != kRefNone;
+        const float4 o4 = slot_ro[slot], d4 = slot_rd[slot];
+        V3 o{o4.x, o4.y, o4.z}, d{d4.x, d4.y, d4.z};
+        if (shade_step(S, rp.max_depth, h, o, d, T, L, k, rng, lc, nbounces)) {
+          slot_ro[slot] = make_float4(o.x, o.y, o.z, 0.0f);
+          slot_rd[slot] = make_float4(d.x, d.y, d.z, 0.0f);
+          trav_init(tin, t, slot, INFINITY);
+        } else {
+          results[MRT_IDX(S, g, rp.G, 21)] = make_float4(L.x, L.y, L.z, __uint_as_float(k));
+          nsamples += 1;
+          g = kIdle;
+        }
+      }
+    }
+  }
+  if (COUNT) flush_counters(cnt, lc, seg, nh, nsamples, nbounces);
 }
 
 // Image::merge in sample order: acc = ((acc + s0) + s1) + ...
@@ -537,6 +635,11 @@ struct mrt_ctx {
   uint32_t trace_grid_alpha = 1024, trace_grid_noalpha = 1024;  // (set from the CU count and occupancy)
   bool scene_alpha = true;  // the scene has alpha-tested triangles
   TraceTune tune;
+  // k_render: per-lane current world ray; event pair timing one launch
+  float4* slot_ro = nullptr;
+  float4* slot_rd = nullptr;
+  size_t slots_cap = 0;
+  hipEvent_t tev[2] = {nullptr, nullptr};
   // Live paths per iteration (MRT_POOL_PATHS overrides). Large on purpose:
   // every k_trace launch ends with a tail of long rays on few lanes, so the
   // more rays a launch carries the smaller that tail's share (measured on
@@ -660,6 +763,16 @@ void ensure_results(mrt_ctx* c, size_t n) {
   c->results_cap = n;
 }
 
+void ensure_slots(mrt_ctx* c, size_t n) {
+  if (n <= c->slots_cap) return;
+  if (c->slot_ro) HIP_CHECK(hipFree(c->slot_ro));
+  c->slot_ro = nullptr;
+  c->slot_rd = nullptr;
+  HIP_CHECK(hipMalloc(&c->slot_ro, 32 * n));
+  c->slot_rd = c->slot_ro + n;
+  c->slots_cap = n;
+}
+
 std::pair<uint32_t*, uint32_t> pixlist(mrt_ctx* c, uint32_t W, uint32_t H, uint32_t si, uint32_t sc) {
   auto key = std::make_tuple(W, H, si, sc);
   auto it = c->pixlists.find(key);
@@ -686,6 +799,77 @@ std::pair<uint32_t*, uint32_t> pixlist(mrt_ctx* c, uint32_t W, uint32_t H, uint3
   return v;
 }
 
+// Occupancy-sized persistent grid for kernel f with `smem` dynamic LDS.
+uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem) {
+  int per_cu = 0;
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, smem));
+  if (const char* e = getenv("MRT_TRACE_WGS_PER_CU")) per_cu = atoi(e);
+  return (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
+}
+
+template <bool LDS, bool ALPHA>
+void launch_render_v(mrt_ctx* c, hipStream_t st, const RenderParams& rp, bool count) {
+  const size_t smem = LDS ? (size_t)c->S.n_slots * 16 : 0;
+  const void* f = count ? (const void*)k_render<true, LDS, ALPHA> : (const void*)k_render<false, LDS, ALPHA>;
+  const uint32_t grid = persistent_grid(c, f, smem);
+  ensure_slots(c, (size_t)grid * kBlock);
+  if (count)
+    hipLaunchKernelGGL((k_render<true, LDS, ALPHA>), dim3(grid), dim3(kBlock), smem, st, c->S, c->cam, rp, c->slot_ro,
+                       c->slot_rd, c->ctrl, c->results, c->d_cnt, c->tune);
+  else
+    hipLaunchKernelGGL((k_render<false, LDS, ALPHA>), dim3(grid), dim3(kBlock), smem, st, c->S, c->cam, rp,
+                       c->slot_ro, c->slot_rd, c->ctrl, c->results, c->d_cnt, c->tune);
+  HIP_CHECK(hipGetLastError());
+}
+
+// The fused path loop: one k_render launch + one k_accumulate per chunk.
+void render_fused(mrt_ctx* c, const mrt_render_args* a, const uint32_t* pixlist_d, uint32_t n_pix, uint32_t spp_chunk,
+                  float* d_rgb, uint32_t* d_b, hipStream_t st) {
+  const bool count = (a->flags & MRT_RENDER_COUNTERS) != 0;
+  const bool timing = (a->flags & MRT_RENDER_TIME_KERNELS) != 0;
+  ensure_results(c, (size_t)n_pix * spp_chunk);
+  for (uint32_t done = 0; done < a->spp_count; done += spp_chunk) {
+    const uint32_t cs = std::min(spp_chunk, a->spp_count - done);
+    if (a->max_depth == 0) continue;  // trace(ray, 0) returns (0, 0): nothing to add
+    RenderParams rp;
+    rp.W = a->width;
+    rp.H = a->height;
+    rp.seed = a->seed;
+    rp.max_depth = a->max_depth;
+    rp.n_pix = n_pix;
+    rp.G = n_pix * cs;
+    rp.sample_base = a->spp_begin + done;
+    rp.pixlist = pixlist_d;
+    rp.pool_cap = 0;
+    Ctrl init{{0, 0}, 0, 0};
+    HIP_CHECK(hipMemcpyAsync(c->ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, st));
+    if (timing) HIP_CHECK(hipEventRecord(c->tev[0], st));
+    if (c->trace_lds) {
+      if (c->scene_alpha)
+        launch_render_v<true, true>(c, st, rp, count);
+      else
+        launch_render_v<true, false>(c, st, rp, count);
+    } else {
+      if (c->scene_alpha)
+        launch_render_v<false, true>(c, st, rp, count);
+      else
+        launch_render_v<false, false>(c, st, rp, count);
+    }
+    if (timing) {
+      HIP_CHECK(hipEventRecord(c->tev[1], st));
+      HIP_CHECK(hipEventSynchronize(c->tev[1]));
+      float ms = 0;
+      HIP_CHECK(hipEventElapsedTime(&ms, c->tev[0], c->tev[1]));
+      c->kstats.trace_ms += ms;
+      c->kstats.trace_launches++;
+      c->kstats.iterations++;
+    }
+    hipLaunchKernelGGL(k_accumulate, dim3((n_pix + kBlock - 1) / kBlock), dim3(kBlock), 0, st, (const float4*)c->results,
+                       n_pix, cs, pixlist_d, d_rgb, d_b);
+    HIP_CHECK(hipGetLastError());
+  }
+}
+
 void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t* d_b, hipStream_t st) {
   if (!a) throw ApiError{MRT_ERR_INVALID, "null render args"};
   if (!c->has_scene) throw ApiError{MRT_ERR_STATE, "no scene uploaded"};
@@ -702,6 +886,10 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
   const bool count = (a->flags & MRT_RENDER_COUNTERS) != 0;
   // results slab <= kResultsMax samples (16 B each); pool <= c->pool_paths
   uint32_t spp_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(a->spp_count, kResultsMax / n_pix));
+  if ((a->flags & MRT_RENDER_FUSED) && !(a->flags & MRT_RENDER_SIMPLE_TRACE)) {
+    render_fused(c, a, pl.first, n_pix, spp_chunk, d_rgb, d_b, st);
+    return;
+  }
   const size_t pool = std::min<size_t>((size_t)n_pix * spp_chunk, c->pool_paths);
   ensure_pool(c, pool);
   ensure_results(c, (size_t)n_pix * spp_chunk);
@@ -842,6 +1030,8 @@ int mrt_create(int device, mrt_ctx** out) {
     HIP_CHECK(hipHostMalloc(&c->h_status, 2 * sizeof(Ctrl), hipHostMallocDefault));
     HIP_CHECK(hipEventCreateWithFlags(&c->ev[0], hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&c->ev[1], hipEventDisableTiming));
+    HIP_CHECK(hipEventCreate(&c->tev[0]));
+    HIP_CHECK(hipEventCreate(&c->tev[1]));
     int cus = 0;
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     // persistent k_trace: as many resident workgroups as the register budget
@@ -853,6 +1043,7 @@ int mrt_create(int device, mrt_ctx** out) {
     if (const char* e = getenv("MRT_TRACE_REFILL")) c->tune.refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_PRIM_BATCH")) c->tune.prim_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_CHUNK")) c->tune.chunk = (uint32_t)std::max(64, atoi(e));
+    if (const char* e = getenv("MRT_SHADE_BATCH")) c->tune.shade_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_POOL_PATHS")) c->pool_paths = (size_t)std::max(1 << 16, std::min(1 << 28, atoi(e)));
     c->trace_grid_alpha = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
     HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false, false>, kBlock, 0));
@@ -885,10 +1076,13 @@ int mrt_destroy(mrt_ctx* c) {
   hipFree(c->d_acc_b);
   hipFree(c->d_rays);
   hipFree(c->d_rhits);
+  hipFree(c->slot_ro);
   for (auto& kv : c->pixlists) hipFree(kv.second.first);
   if (c->h_status) hipHostFree(c->h_status);
   if (c->ev[0]) hipEventDestroy(c->ev[0]);
   if (c->ev[1]) hipEventDestroy(c->ev[1]);
+  if (c->tev[0]) hipEventDestroy(c->tev[0]);
+  if (c->tev[1]) hipEventDestroy(c->tev[1]);
   for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;

@@ -34,6 +34,7 @@ NO_MATERIAL = 0xFFFFFFFF
 RENDER_COUNTERS = 1
 RENDER_TIME_KERNELS = 2
 RENDER_SIMPLE_TRACE = 4  # debug: one-ray-per-thread closest hit (bisection aid)
+RENDER_FUSED = 8  # one persistent k_render instead of the k_trace/k_shade loop (same results)
 MAX_DEPTH = 50  # main.rs:37
 ASPECT_RATIO = np.float32(16.0) / np.float32(9.0)  # main.rs:39 (f32)
 

@@ -270,6 +270,9 @@ def test_trace_rays_model_blas_random(ctx, variant):
     rgb, bo = ctx.render(32, 18, 0, 2, seed=5)
     rgb2, bo2 = ctx.render(32, 18, 0, 2, seed=5, flags=massrt.RENDER_SIMPLE_TRACE)
     assert np.array_equal(bo, bo2) and np.array_equal(rgb, rgb2)
+    # and so does the fused persistent kernel
+    rgb3, bo3 = ctx.render(32, 18, 0, 2, seed=5, flags=massrt.RENDER_FUSED)
+    assert np.array_equal(bo, bo3) and np.array_equal(rgb, rgb3)
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
