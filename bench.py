@@ -192,6 +192,7 @@ def main():
             "avg_launch_ms": round(ks["trace_ms"] / ks["trace_launches"], 4),
             "launches": int(ks["trace_launches"]), "bytes_per_segment": round(bytes_per_seg, 1),
             "segments_per_sample": round(seg_per_sample, 4),
+            "lane_utilisation": round(cnt["lane_steps"] / max(cnt["wave_slots"], 1), 4),
         }
 
     cpu = None

@@ -211,6 +211,11 @@ typedef struct {
   uint64_t closest_hits;
   uint64_t texel_taps;
   uint64_t bounces;
+  /* scheduling efficiency of the persistent k_trace (not reference quantities):
+   * wave_slots = loop iterations x 64 lanes, lane_steps = box/primitive steps
+   * executed; lane_steps / wave_slots = SIMD lane utilisation */
+  uint64_t wave_slots;
+  uint64_t lane_steps;
 } mrt_counters;
 
 /* Kernel timing accumulated by renders flagged MRT_RENDER_TIME_KERNELS

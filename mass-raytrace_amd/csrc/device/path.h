@@ -27,12 +27,12 @@ MRT_DEV uint32_t make_ref(uint32_t kind, uint32_t idx) { return (kind << 28) | i
 
 struct DevCounters {
   unsigned long long samples, segments, node_visits, sphere_tests, triangle_tests, instance_entries,
-      model_entries, closest_hits, texel_taps, bounces;
+      model_entries, closest_hits, texel_taps, bounces, wave_slots, lane_steps;
 };
 
 struct LocalCounters {
   uint32_t node_visits = 0, sphere_tests = 0, triangle_tests = 0, instance_entries = 0, model_entries = 0,
-           texel_taps = 0;
+           texel_taps = 0, wave_slots = 0, lane_steps = 0;
 };
 
 // Bounds checks of every scene-array index, compiled in with

@@ -108,11 +108,11 @@ __device__ __forceinline__ uint32_t wg_reserve(uint32_t* counter, uint32_t count
 
 __device__ void flush_counters(DevCounters* c, const LocalCounters& lc, uint32_t segs, uint32_t hits,
                                uint32_t samples, uint32_t bounces) {
-  uint32_t v[10] = {samples, segs, lc.node_visits, lc.sphere_tests, lc.triangle_tests, lc.instance_entries,
-                    lc.model_entries, hits, lc.texel_taps, bounces};
+  uint32_t v[12] = {samples, segs, lc.node_visits, lc.sphere_tests, lc.triangle_tests, lc.instance_entries,
+                    lc.model_entries, hits, lc.texel_taps, bounces, lc.wave_slots, lc.lane_steps};
   unsigned long long* dst = reinterpret_cast<unsigned long long*>(c);
 #pragma unroll
-  for (int k = 0; k < 10; ++k) {
+  for (int k = 0; k < 12; ++k) {
     uint32_t s = wave_sum(v[k]);
     if (lane_id() == 0 && s) atomicAdd(dst + k, (unsigned long long)s);
   }
@@ -167,7 +167,10 @@ struct TraceTune {
 constexpr size_t kTraceLdsMaxBytes = 64 * 1024;
 constexpr uint32_t kIdle = 0xFFFFFFFFu;  // Trav.ray of a lane without a ray
 
-template <bool COUNT, bool LDS, bool ALPHA>
+// R > 1: each lane interleaves R independent rays (software ILP) — while one
+// ray's record fetch is in flight the lane steps the other, doubling the
+// memory-level parallelism a wave offers at the price of more registers.
+template <bool COUNT, bool LDS, bool ALPHA, int R>
 __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   DevCounters* cnt, float tmin, float tmax, TraceTune tune) {
   extern __shared__ uint4 lds_slots[];
@@ -184,13 +187,22 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
   uint32_t seg = 0, nh = 0;
   uint32_t pool = 0, pool_end = 0;  // wave-uniform chunk [pool, pool_end)
   bool drained = false;             // wave-uniform: the counter passed n
-  Trav t{};  // fully initialised: idle lanes must not carry undefined state
-  t.done = true;
-  t.ray = kIdle;
+  Trav t[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    t[q] = Trav{};  // fully initialised: idle lanes must not carry undefined state
+    t[q].done = true;
+    t[q].ray = kIdle;
+  }
   for (;;) {
-    const unsigned long long idle = __ballot(t.ray == kIdle);
-    const uint32_t n_idle = (uint32_t)__popcll(idle);
-    if (n_idle >= tune.refill || n_idle == 64) {
+    unsigned long long idle[R];
+    uint32_t n_idle = 0;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      idle[q] = __ballot(t[q].ray == kIdle);
+      n_idle += (uint32_t)__popcll(idle[q]);
+    }
+    if (n_idle >= tune.refill * R || n_idle == 64u * R) {
       if (pool == pool_end && !drained) {  // grab the next chunk (wave-uniform)
         uint32_t b = 0;
         if (lane_id() == 0) b = atomicAdd(&ctrl->trace_next, tune.chunk);
@@ -200,26 +212,44 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
         drained = b + tune.chunk >= n;
       }
       const uint32_t avail = pool_end - pool;
-      if (t.ray == kIdle) {
-        const uint32_t r = lane_rank(idle);
-        if (r < avail) trav_init(tin, t, MRT_IDX(S, pool + r, n, 20), tmax);
+      uint32_t off = 0;
+      unsigned long long live = 0;
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        if (t[q].ray == kIdle) {
+          const uint32_t r = off + lane_rank(idle[q]);
+          if (r < avail) trav_init(tin, t[q], MRT_IDX(S, pool + r, n, 20), tmax);
+        }
+        off += (uint32_t)__popcll(idle[q]);
+        live |= __ballot(t[q].ray != kIdle);
       }
       pool += n_idle < avail ? n_idle : avail;
-      if (__ballot(t.ray != kIdle) == 0) break;  // chunk source exhausted
+      if (live == 0) break;  // chunk source exhausted
     }
-    const bool busy = !t.done;  // idle lanes hold a done Trav
-    const bool at_box = busy && trav_at_box(t);
-    const unsigned long long box_mask = __ballot(at_box);
-    const unsigned long long prim_mask = __ballot(busy && !at_box);
-    if (at_box) trav_box<COUNT>(tin, t, lc);
-    // primitives wait until enough lanes are at one (or no lane is at a box)
-    if ((__popcll(prim_mask) >= tune.prim_batch || box_mask == 0) && busy && !at_box) trav_prim<COUNT, ALPHA>(tin, t, lc);
-    if (t.ray != kIdle && t.done) {
-      const Hit h = trav_hit(tin, t);
-      hits[t.ray] = make_uint4(__float_as_uint(h.t), h.prim, h.container, 0u);
-      seg += 1;
-      nh += t.prim != kRefNone;
-      t.ray = kIdle;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const bool busy = !t[q].done;  // idle lanes hold a done Trav
+      const bool at_box = busy && trav_at_box(t[q]);
+      const unsigned long long box_mask = __ballot(at_box);
+      const unsigned long long prim_mask = __ballot(busy && !at_box);
+      if (at_box) trav_box<COUNT>(tin, t[q], lc);
+      // primitives wait until enough lanes are at one (or no lane is at a box)
+      const bool prim_go = (__popcll(prim_mask) >= tune.prim_batch || box_mask == 0) && busy && !at_box;
+      if (prim_go) trav_prim<COUNT, ALPHA>(tin, t[q], lc);
+      if (COUNT) {
+        lc.wave_slots += lane_id() == 0 ? 64u : 0u;
+        lc.lane_steps += (at_box || prim_go) ? 1u : 0u;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      if (t[q].ray != kIdle && t[q].done) {
+        const Hit h = trav_hit(tin, t[q]);
+        hits[t[q].ray] = make_uint4(__float_as_uint(h.t), h.prim, h.container, 0u);
+        seg += 1;
+        nh += t[q].prim != kRefNone;
+        t[q].ray = kIdle;
+      }
     }
   }
   if (COUNT) flush_counters(cnt, lc, seg, nh, 0, 0);
@@ -631,8 +661,9 @@ struct mrt_ctx {
   uint32_t* dbg = nullptr;  // MRT_DEBUG_BOUNDS record (4 words)
   Ctrl* h_status = nullptr;  // pinned, 2 slots
   hipEvent_t ev[2]{};
-  uint32_t trace_grid = 1024;  // persistent k_trace workgroups of the current scene's variant
-  uint32_t trace_grid_alpha = 1024, trace_grid_noalpha = 1024;  // (set from the CU count and occupancy)
+  uint32_t trace_grid = 1024;  // k_trace_simple workgroups
+  int rays_per_lane = 1;       // k_trace R (MRT_TRACE_RAYS_PER_LANE)
+  std::map<std::pair<const void*, size_t>, uint32_t> grids;  // persistent grid per (kernel, LDS bytes)
   bool scene_alpha = true;  // the scene has alpha-tested triangles
   TraceTune tune;
   // k_render: per-lane current world ray; event pair timing one launch
@@ -648,7 +679,7 @@ struct mrt_ctx {
   size_t pool_paths = (size_t)64 << 20;
   int cus = 1;
   bool trace_lds = false;          // record stream staged in LDS (set per scene)
-  uint32_t trace_grid_lds = 1024;  // workgroups of the LDS variant
+
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t*, uint32_t>> pixlists;
   // host-buffer render staging
   float* d_acc_rgb = nullptr;
@@ -704,17 +735,41 @@ size_t align_up(size_t x) {
 // The persistent closest-hit kernel over pool buffer `in`, specialised on
 // the scene (record stream in LDS when it fits; alpha test compiled in only
 // when the scene has alpha-textured triangles).
+// Occupancy-sized persistent grid for kernel f with `smem` dynamic LDS.
+uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem) {
+  auto key = std::make_pair(f, smem);
+  auto it = c->grids.find(key);
+  if (it != c->grids.end()) return it->second;
+  if (smem > 0) HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTraceLdsMaxBytes));
+  int per_cu = 0;
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, smem));
+  if (const char* e = getenv("MRT_TRACE_WGS_PER_CU")) per_cu = atoi(e);
+  const uint32_t g = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
+  c->grids[key] = g;
+  return g;
+}
+
+template <bool LDS, bool ALPHA, int R>
+void launch_trace_r(mrt_ctx* c, hipStream_t st, const PathBufs& in, uint32_t cur, bool count, float tmin,
+                    float tmax) {
+  const size_t smem = LDS ? (size_t)c->S.n_slots * 16 : 0;
+  const void* f = count ? (const void*)k_trace<true, LDS, ALPHA, R> : (const void*)k_trace<false, LDS, ALPHA, R>;
+  const uint32_t grid = persistent_grid(c, f, smem);
+  if (count)
+    hipLaunchKernelGGL((k_trace<true, LDS, ALPHA, R>), dim3(grid), dim3(kBlock), smem, st, c->S, in, c->hits,
+                       c->ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
+  else
+    hipLaunchKernelGGL((k_trace<false, LDS, ALPHA, R>), dim3(grid), dim3(kBlock), smem, st, c->S, in, c->hits,
+                       c->ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
+}
+
 template <bool LDS, bool ALPHA>
 void launch_trace_v(mrt_ctx* c, hipStream_t st, const PathBufs& in, uint32_t cur, bool count, float tmin,
                     float tmax) {
-  const size_t smem = LDS ? (size_t)c->S.n_slots * 16 : 0;
-  const dim3 grid(LDS ? c->trace_grid_lds : c->trace_grid);
-  if (count)
-    hipLaunchKernelGGL((k_trace<true, LDS, ALPHA>), grid, dim3(kBlock), smem, st, c->S, in, c->hits, c->ctrl, cur,
-                       c->d_cnt, tmin, tmax, c->tune);
+  if (c->rays_per_lane == 2)
+    launch_trace_r<LDS, ALPHA, 2>(c, st, in, cur, count, tmin, tmax);
   else
-    hipLaunchKernelGGL((k_trace<false, LDS, ALPHA>), grid, dim3(kBlock), smem, st, c->S, in, c->hits, c->ctrl, cur,
-                       c->d_cnt, tmin, tmax, c->tune);
+    launch_trace_r<LDS, ALPHA, 1>(c, st, in, cur, count, tmin, tmax);
 }
 
 void launch_trace(mrt_ctx* c, hipStream_t st, const PathBufs& in, uint32_t cur, bool count, float tmin, float tmax) {
@@ -799,13 +854,6 @@ std::pair<uint32_t*, uint32_t> pixlist(mrt_ctx* c, uint32_t W, uint32_t H, uint3
   return v;
 }
 
-// Occupancy-sized persistent grid for kernel f with `smem` dynamic LDS.
-uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem) {
-  int per_cu = 0;
-  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, smem));
-  if (const char* e = getenv("MRT_TRACE_WGS_PER_CU")) per_cu = atoi(e);
-  return (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
-}
 
 template <bool LDS, bool ALPHA>
 void launch_render_v(mrt_ctx* c, hipStream_t st, const RenderParams& rp, bool count) {
@@ -1034,24 +1082,14 @@ int mrt_create(int device, mrt_ctx** out) {
     HIP_CHECK(hipEventCreate(&c->tev[1]));
     int cus = 0;
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-    // persistent k_trace: as many resident workgroups as the register budget
-    // allows on every CU (MRT_TRACE_WGS_PER_CU overrides, for tuning)
-    int per_cu = 0;
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false, true>, kBlock, 0));
-    if (const char* e = getenv("MRT_TRACE_WGS_PER_CU")) per_cu = atoi(e);
     c->cus = std::max(1, cus);
+    c->trace_grid = (uint32_t)c->cus * 4;  // k_trace_simple (debug)
     if (const char* e = getenv("MRT_TRACE_REFILL")) c->tune.refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_PRIM_BATCH")) c->tune.prim_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_CHUNK")) c->tune.chunk = (uint32_t)std::max(64, atoi(e));
     if (const char* e = getenv("MRT_SHADE_BATCH")) c->tune.shade_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_POOL_PATHS")) c->pool_paths = (size_t)std::max(1 << 16, std::min(1 << 28, atoi(e)));
-    c->trace_grid_alpha = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false, false>, kBlock, 0));
-    if (const char* e = getenv("MRT_TRACE_WGS_PER_CU")) per_cu = atoi(e);
-    c->trace_grid_noalpha = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
-    for (auto f : {(const void*)k_trace<false, true, false>, (const void*)k_trace<true, true, false>,
-                   (const void*)k_trace<false, true, true>, (const void*)k_trace<true, true, true>})
-      HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTraceLdsMaxBytes));
+    if (const char* e = getenv("MRT_TRACE_RAYS_PER_LANE")) c->rays_per_lane = atoi(e) == 2 ? 2 : 1;
   });
   if (rc != MRT_OK) {
     g_last_error = c->err;
@@ -1160,15 +1198,6 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     const char* no_lds = getenv("MRT_TRACE_LDS");
     c->trace_lds = lds_bytes <= kTraceLdsMaxBytes && !(no_lds && no_lds[0] == '0');
     c->scene_alpha = hs.has_alpha;
-    c->trace_grid = c->scene_alpha ? c->trace_grid_alpha : c->trace_grid_noalpha;
-    if (c->trace_lds) {
-      int per_cu = 0;
-      if (c->scene_alpha)
-        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, true, true>, kBlock, lds_bytes));
-      else
-        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, true, false>, kBlock, lds_bytes));
-      c->trace_grid_lds = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
-    }
     c->has_scene = true;
   });
 }
@@ -1280,6 +1309,8 @@ int mrt_get_counters(mrt_ctx* c, mrt_counters* out) {
     out->closest_hits = h.closest_hits;
     out->texel_taps = h.texel_taps;
     out->bounces = h.bounces;
+    out->wave_slots = h.wave_slots;
+    out->lane_steps = h.lane_steps;
   });
 }
 

@@ -139,11 +139,15 @@ class MrtKernelStats(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+# scheduling counters of the persistent k_trace (no reference counterpart)
+SCHED_FIELDS = ["wave_slots", "lane_steps"]
+
+
 class MrtCounters(C.Structure):
-    _fields_ = [(f, C.c_uint64) for f in COUNTER_FIELDS]
+    _fields_ = [(f, C.c_uint64) for f in COUNTER_FIELDS + SCHED_FIELDS]
 
     def as_dict(self) -> dict:
-        return {f: int(getattr(self, f)) for f in COUNTER_FIELDS}
+        return {f: int(getattr(self, f)) for f in COUNTER_FIELDS + SCHED_FIELDS}
 
 
 # symbols the header declares (checked by the CPU test-suite)
