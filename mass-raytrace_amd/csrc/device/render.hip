@@ -132,12 +132,14 @@ __device__ __forceinline__ void gen_work(const DevCamera& cam, const RenderParam
   rs = make_uint4((uint32_t)rng.s0, (uint32_t)(rng.s0 >> 32), (uint32_t)rng.s1, (uint32_t)(rng.s1 >> 32));
 }
 
-__global__ __launch_bounds__(kBlock) void k_generate(DevCamera cam, RenderParams rp, PathBufs out, uint32_t n0) {
+// Initial pool: work items [base, base + n0) into slots [0, n0).
+__global__ __launch_bounds__(kBlock) void k_generate(DevCamera cam, RenderParams rp, PathBufs out, uint32_t base,
+                                                     uint32_t n0) {
   uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n0) return;
   float4 ro, rd;
   uint4 rs;
-  gen_work(cam, rp, i, ro, rd, rs);
+  gen_work(cam, rp, base + i, ro, rd, rs);
   out.ro[i] = ro;
   out.rd[i] = rd;
   out.thr[i] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
@@ -299,7 +301,7 @@ MRT_DEV bool shade_step(const DevScene& S, uint32_t max_depth, const Hit& h, V3&
 template <bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, DevCamera cam, RenderParams rp, PathBufs in,
                                                   PathBufs out, const uint4* hits, Ctrl* ctrl, uint32_t cur,
-                                                  float4* results, DevCounters* cnt) {
+                                                  uint32_t* work, float4* results, DevCounters* cnt) {
   const uint32_t n = ctrl->active[cur];
   if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->trace_next = 0;  // k_trace of the next iteration
   const uint32_t base = blockIdx.x * kBlock;
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, DevCamera cam, Ren
   __shared__ uint32_t s_cnt[kWaves], s_base;
   const uint32_t wave = threadIdx.x / 64;
   const unsigned long long need_mask = __ballot(need);
-  const uint32_t wbase = wg_reserve(&ctrl->next_work, (uint32_t)__popcll(need_mask), wave, s_cnt, s_base);
+  const uint32_t wbase = wg_reserve(work, (uint32_t)__popcll(need_mask), wave, s_cnt, s_base);
   if (need) {
     uint32_t g = wbase + lane_rank(need_mask);
     if (g < rp.G) {
@@ -638,6 +640,23 @@ __global__ __launch_bounds__(kBlock) void k_selftest_slab(unsigned long long n, 
 }  // namespace
 
 // ---------------------------------------------------------------------------
+// One independent path pool driven on its own stream. Several queues share
+// the work counter and run concurrently, so one queue's k_trace tail (the
+// last long rays on few lanes) overlaps the other queues' kernels instead of
+// idling the GPU.
+constexpr int kMaxQueues = 4;
+struct Queue {
+  hipStream_t stream = nullptr;
+  PathBufs bufs[2]{};
+  uint4* hits = nullptr;
+  size_t cap = 0;
+  Ctrl* ctrl = nullptr;        // device
+  Ctrl* h_status = nullptr;    // pinned, 2 slots (lagged status reads)
+  uint32_t* h_work = nullptr;  // pinned, 2 slots: snapshots of the shared work counter
+  hipEvent_t ev[2]{};
+  hipEvent_t join = nullptr;
+};
+
 struct mrt_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -650,17 +669,16 @@ struct mrt_ctx {
   DevCamera cam{};
   bool has_camera = false;
   // render state
-  size_t pool_cap = 0;
+  size_t pool_cap = 0;  // paths over all queues
   void* pool_mem = nullptr;
-  PathBufs bufs[2]{};
-  uint4* hits = nullptr;
+  Queue q[kMaxQueues];
+  int n_queues = 2;            // MRT_QUEUES overrides (1..4)
+  uint32_t* work = nullptr;    // shared work counter of the wavefront loop
+  hipEvent_t fork = nullptr;
   float4* results = nullptr;
   size_t results_cap = 0;
-  Ctrl* ctrl = nullptr;
   DevCounters* d_cnt = nullptr;
   uint32_t* dbg = nullptr;  // MRT_DEBUG_BOUNDS record (4 words)
-  Ctrl* h_status = nullptr;  // pinned, 2 slots
-  hipEvent_t ev[2]{};
   uint32_t trace_grid = 1024;  // k_trace_simple workgroups
   int rays_per_lane = 1;       // k_trace R (MRT_TRACE_RAYS_PER_LANE)
   std::map<std::pair<const void*, size_t>, uint32_t> grids;  // persistent grid per (kernel, LDS bytes)
@@ -735,6 +753,12 @@ size_t align_up(size_t x) {
 // The persistent closest-hit kernel over pool buffer `in`, specialised on
 // the scene (record stream in LDS when it fits; alpha test compiled in only
 // when the scene has alpha-textured triangles).
+// `st` waits for the wavefront queues' last render (their buffers are reused).
+void wait_queues(mrt_ctx* c, hipStream_t st) {
+  for (Queue& q : c->q)
+    if (q.join) HIP_CHECK(hipStreamWaitEvent(st, q.join, 0));
+}
+
 // Occupancy-sized persistent grid for kernel f with `smem` dynamic LDS.
 uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem) {
   auto key = std::make_pair(f, smem);
@@ -750,39 +774,40 @@ uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem) {
 }
 
 template <bool LDS, bool ALPHA, int R>
-void launch_trace_r(mrt_ctx* c, hipStream_t st, const PathBufs& in, uint32_t cur, bool count, float tmin,
-                    float tmax) {
+void launch_trace_r(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
+                    float tmin, float tmax) {
   const size_t smem = LDS ? (size_t)c->S.n_slots * 16 : 0;
   const void* f = count ? (const void*)k_trace<true, LDS, ALPHA, R> : (const void*)k_trace<false, LDS, ALPHA, R>;
   const uint32_t grid = persistent_grid(c, f, smem);
   if (count)
-    hipLaunchKernelGGL((k_trace<true, LDS, ALPHA, R>), dim3(grid), dim3(kBlock), smem, st, c->S, in, c->hits,
-                       c->ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
+    hipLaunchKernelGGL((k_trace<true, LDS, ALPHA, R>), dim3(grid), dim3(kBlock), smem, st, c->S, in, q.hits,
+                       q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
   else
-    hipLaunchKernelGGL((k_trace<false, LDS, ALPHA, R>), dim3(grid), dim3(kBlock), smem, st, c->S, in, c->hits,
-                       c->ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
+    hipLaunchKernelGGL((k_trace<false, LDS, ALPHA, R>), dim3(grid), dim3(kBlock), smem, st, c->S, in, q.hits,
+                       q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
 }
 
 template <bool LDS, bool ALPHA>
-void launch_trace_v(mrt_ctx* c, hipStream_t st, const PathBufs& in, uint32_t cur, bool count, float tmin,
-                    float tmax) {
+void launch_trace_v(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
+                    float tmin, float tmax) {
   if (c->rays_per_lane == 2)
-    launch_trace_r<LDS, ALPHA, 2>(c, st, in, cur, count, tmin, tmax);
+    launch_trace_r<LDS, ALPHA, 2>(c, st, q, in, cur, count, tmin, tmax);
   else
-    launch_trace_r<LDS, ALPHA, 1>(c, st, in, cur, count, tmin, tmax);
+    launch_trace_r<LDS, ALPHA, 1>(c, st, q, in, cur, count, tmin, tmax);
 }
 
-void launch_trace(mrt_ctx* c, hipStream_t st, const PathBufs& in, uint32_t cur, bool count, float tmin, float tmax) {
+void launch_trace(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
+                  float tmin, float tmax) {
   if (c->trace_lds) {
     if (c->scene_alpha)
-      launch_trace_v<true, true>(c, st, in, cur, count, tmin, tmax);
+      launch_trace_v<true, true>(c, st, q, in, cur, count, tmin, tmax);
     else
-      launch_trace_v<true, false>(c, st, in, cur, count, tmin, tmax);
+      launch_trace_v<true, false>(c, st, q, in, cur, count, tmin, tmax);
   } else {
     if (c->scene_alpha)
-      launch_trace_v<false, true>(c, st, in, cur, count, tmin, tmax);
+      launch_trace_v<false, true>(c, st, q, in, cur, count, tmin, tmax);
     else
-      launch_trace_v<false, false>(c, st, in, cur, count, tmin, tmax);
+      launch_trace_v<false, false>(c, st, q, in, cur, count, tmin, tmax);
   }
   HIP_CHECK(hipGetLastError());
 }
@@ -791,23 +816,30 @@ void ensure_pool(mrt_ctx* c, size_t P) {
   if (P <= c->pool_cap) return;
   if (c->pool_mem) HIP_CHECK(hipFree(c->pool_mem));
   c->pool_mem = nullptr;
-  size_t per = 16 * (2 * 5 + 1);  // two state sets + hits
-  HIP_CHECK(hipMalloc(&c->pool_mem, per * P + 4096));
+  c->pool_cap = 0;
+  const int K = c->n_queues;
+  const size_t per_q = (P + K - 1) / K;
+  const size_t per = 16 * (2 * 5 + 1);  // two state sets + hits
+  HIP_CHECK(hipMalloc(&c->pool_mem, (per * per_q + 4096) * K));
   char* p = (char*)c->pool_mem;
   auto take = [&](size_t bytes) {
     char* r = p;
     p += (bytes + 255) & ~(size_t)255;
     return r;
   };
-  for (int b = 0; b < 2; ++b) {
-    c->bufs[b].ro = (float4*)take(16 * P);
-    c->bufs[b].rd = (float4*)take(16 * P);
-    c->bufs[b].thr = (float4*)take(16 * P);
-    c->bufs[b].rad = (float4*)take(16 * P);
-    c->bufs[b].rng = (uint4*)take(16 * P);
+  for (int k = 0; k < K; ++k) {
+    Queue& q = c->q[k];
+    for (int b = 0; b < 2; ++b) {
+      q.bufs[b].ro = (float4*)take(16 * per_q);
+      q.bufs[b].rd = (float4*)take(16 * per_q);
+      q.bufs[b].thr = (float4*)take(16 * per_q);
+      q.bufs[b].rad = (float4*)take(16 * per_q);
+      q.bufs[b].rng = (uint4*)take(16 * per_q);
+    }
+    q.hits = (uint4*)take(16 * per_q);
+    q.cap = per_q;
   }
-  c->hits = (uint4*)take(16 * P);
-  c->pool_cap = P;
+  c->pool_cap = per_q * K;
 }
 
 void ensure_results(mrt_ctx* c, size_t n) {
@@ -863,10 +895,10 @@ void launch_render_v(mrt_ctx* c, hipStream_t st, const RenderParams& rp, bool co
   ensure_slots(c, (size_t)grid * kBlock);
   if (count)
     hipLaunchKernelGGL((k_render<true, LDS, ALPHA>), dim3(grid), dim3(kBlock), smem, st, c->S, c->cam, rp, c->slot_ro,
-                       c->slot_rd, c->ctrl, c->results, c->d_cnt, c->tune);
+                       c->slot_rd, c->q[0].ctrl, c->results, c->d_cnt, c->tune);
   else
     hipLaunchKernelGGL((k_render<false, LDS, ALPHA>), dim3(grid), dim3(kBlock), smem, st, c->S, c->cam, rp,
-                       c->slot_ro, c->slot_rd, c->ctrl, c->results, c->d_cnt, c->tune);
+                       c->slot_ro, c->slot_rd, c->q[0].ctrl, c->results, c->d_cnt, c->tune);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -876,6 +908,7 @@ void render_fused(mrt_ctx* c, const mrt_render_args* a, const uint32_t* pixlist_
   const bool count = (a->flags & MRT_RENDER_COUNTERS) != 0;
   const bool timing = (a->flags & MRT_RENDER_TIME_KERNELS) != 0;
   ensure_results(c, (size_t)n_pix * spp_chunk);
+  wait_queues(c, st);
   for (uint32_t done = 0; done < a->spp_count; done += spp_chunk) {
     const uint32_t cs = std::min(spp_chunk, a->spp_count - done);
     if (a->max_depth == 0) continue;  // trace(ray, 0) returns (0, 0): nothing to add
@@ -890,7 +923,7 @@ void render_fused(mrt_ctx* c, const mrt_render_args* a, const uint32_t* pixlist_
     rp.pixlist = pixlist_d;
     rp.pool_cap = 0;
     Ctrl init{{0, 0}, 0, 0};
-    HIP_CHECK(hipMemcpyAsync(c->ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(c->q[0].ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, st));
     if (timing) HIP_CHECK(hipEventRecord(c->tev[0], st));
     if (c->trace_lds) {
       if (c->scene_alpha)
@@ -941,6 +974,16 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
   const size_t pool = std::min<size_t>((size_t)n_pix * spp_chunk, c->pool_paths);
   ensure_pool(c, pool);
   ensure_results(c, (size_t)n_pix * spp_chunk);
+  const int K = c->n_queues;
+  const bool timing = (a->flags & MRT_RENDER_TIME_KERNELS) != 0;
+  auto next_event = [&]() {
+    if (c->ev_used == c->ev_pool.size()) {
+      hipEvent_t e;
+      HIP_CHECK(hipEventCreate(&e));
+      c->ev_pool.push_back(e);
+    }
+    return c->ev_pool[c->ev_used++];
+  };
   for (uint32_t done = 0; done < a->spp_count; done += spp_chunk) {
     uint32_t cs = std::min(spp_chunk, a->spp_count - done);
     RenderParams rp;
@@ -952,76 +995,96 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
     rp.G = n_pix * cs;
     rp.sample_base = a->spp_begin + done;
     rp.pixlist = pl.first;
-    rp.pool_cap = (uint32_t)c->pool_cap;
+    rp.pool_cap = (uint32_t)c->q[0].cap;
     if (a->max_depth == 0) {
       // trace(ray, 0) returns (0, 0) for every sample: nothing to add
       continue;
     }
-    uint32_t n0 = (uint32_t)std::min<size_t>(rp.G, c->pool_cap);
-    Ctrl init{{n0, 0}, n0, 0};  // trace_next = 0
-    HIP_CHECK(hipMemcpyAsync(c->ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_generate, dim3((n0 + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c->cam, rp, c->bufs[0], n0);
-    HIP_CHECK(hipGetLastError());
-    const uint32_t grid = (uint32_t)((c->pool_cap + kBlock - 1) / kBlock);
-    const bool timing = (a->flags & MRT_RENDER_TIME_KERNELS) != 0;
+    // fork: the queues start after everything already on `st`
+    const uint32_t n0 = (uint32_t)std::min<size_t>(rp.G, c->pool_cap);
+    HIP_CHECK(hipMemcpyAsync(c->work, &n0, 4, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipEventRecord(c->fork, st));
+    uint32_t base = 0;
+    for (int k = 0; k < K; ++k) {
+      Queue& q = c->q[k];
+      const uint32_t nk = (uint32_t)(((uint64_t)n0 * (k + 1)) / K) - base;  // <= q.cap
+      HIP_CHECK(hipStreamWaitEvent(q.stream, c->fork, 0));
+      Ctrl init{{nk, 0}, 0, 0};
+      HIP_CHECK(hipMemcpyAsync(q.ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, q.stream));
+      if (nk) {
+        hipLaunchKernelGGL(k_generate, dim3((nk + kBlock - 1) / kBlock), dim3(kBlock), 0, q.stream, c->cam, rp,
+                           q.bufs[0], base, nk);
+        HIP_CHECK(hipGetLastError());
+      }
+      base += nk;
+    }
+    const uint32_t grid = (uint32_t)((c->q[0].cap + kBlock - 1) / kBlock);
     std::vector<std::array<hipEvent_t, 3>> marks;
-    auto next_event = [&]() {
-      if (c->ev_used == c->ev_pool.size()) {
-        hipEvent_t e;
-        HIP_CHECK(hipEventCreate(&e));
-        c->ev_pool.push_back(e);
-      }
-      return c->ev_pool[c->ev_used++];
-    };
-    const int kBatch = 4;
-    uint32_t it = 0;
-    int slot = 0;
-    bool pending = false;
-    for (;;) {
-      for (int b = 0; b < kBatch; ++b, ++it) {
-        uint32_t cur = it & 1;
-        std::array<hipEvent_t, 3> m{};
-        if (timing) {
-          m[0] = next_event();
-          HIP_CHECK(hipEventRecord(m[0], st));
+    const int kBatch = 4;  // even: a status read sees the live pool in active[0]
+    struct Loop {
+      uint32_t it = 0;
+      int slot = 0;
+      bool pending = false, finished = false;
+    } st_[kMaxQueues];
+    int open = K;
+    while (open > 0) {
+      for (int k = 0; k < K; ++k) {
+        Queue& q = c->q[k];
+        Loop& L = st_[k];
+        if (L.finished) continue;
+        for (int b = 0; b < kBatch; ++b, ++L.it) {
+          const uint32_t cur = L.it & 1;
+          std::array<hipEvent_t, 3> m{};
+          if (timing) {
+            m[0] = next_event();
+            HIP_CHECK(hipEventRecord(m[0], q.stream));
+          }
+          if (a->flags & MRT_RENDER_SIMPLE_TRACE)
+            hipLaunchKernelGGL(k_trace_simple, dim3(c->trace_grid), dim3(kBlock), 0, q.stream, c->S, q.bufs[cur],
+                               q.hits, q.ctrl, cur, c->d_cnt);
+          else
+            launch_trace(c, q.stream, q, q.bufs[cur], cur, count, kTmin, INFINITY);
+          HIP_CHECK(hipGetLastError());
+          if (timing) {
+            m[1] = next_event();
+            HIP_CHECK(hipEventRecord(m[1], q.stream));
+          }
+          if (count)
+            hipLaunchKernelGGL(k_shade<true>, dim3(grid), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, q.bufs[cur],
+                               q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, c->work, c->results, c->d_cnt);
+          else
+            hipLaunchKernelGGL(k_shade<false>, dim3(grid), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, q.bufs[cur],
+                               q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, c->work, c->results, c->d_cnt);
+          HIP_CHECK(hipGetLastError());
+          if (timing) {
+            m[2] = next_event();
+            HIP_CHECK(hipEventRecord(m[2], q.stream));
+            marks.push_back(m);
+          }
         }
-        if (a->flags & MRT_RENDER_SIMPLE_TRACE)
-          hipLaunchKernelGGL(k_trace_simple, dim3(c->trace_grid), dim3(kBlock), 0, st, c->S, c->bufs[cur], c->hits,
-                             c->ctrl, cur, c->d_cnt);
-        else
-          launch_trace(c, st, c->bufs[cur], cur, count, kTmin, INFINITY);
-        HIP_CHECK(hipGetLastError());
-        if (timing) {
-          m[1] = next_event();
-          HIP_CHECK(hipEventRecord(m[1], st));
+        HIP_CHECK(hipMemcpyAsync(&q.h_status[L.slot], q.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, q.stream));
+        HIP_CHECK(hipMemcpyAsync(&q.h_work[L.slot], c->work, 4, hipMemcpyDeviceToHost, q.stream));
+        HIP_CHECK(hipEventRecord(q.ev[L.slot], q.stream));
+        if (L.pending) {  // the previous batch's status (one batch stays in flight)
+          HIP_CHECK(hipEventSynchronize(q.ev[L.slot ^ 1]));
+          const Ctrl& s = q.h_status[L.slot ^ 1];
+          if (s.active[0] == 0 && q.h_work[L.slot ^ 1] >= rp.G) {
+            L.finished = true;
+            --open;
+          }
         }
-        if (count)
-          hipLaunchKernelGGL(k_shade<true>, dim3(grid), dim3(kBlock), 0, st, c->S, c->cam, rp, c->bufs[cur],
-                             c->bufs[cur ^ 1], (const uint4*)c->hits, c->ctrl, cur, c->results, c->d_cnt);
-        else
-          hipLaunchKernelGGL(k_shade<false>, dim3(grid), dim3(kBlock), 0, st, c->S, c->cam, rp, c->bufs[cur],
-                             c->bufs[cur ^ 1], (const uint4*)c->hits, c->ctrl, cur, c->results, c->d_cnt);
-        HIP_CHECK(hipGetLastError());
-        if (timing) {
-          m[2] = next_event();
-          HIP_CHECK(hipEventRecord(m[2], st));
-          marks.push_back(m);
-        }
+        L.pending = true;
+        L.slot ^= 1;
+        if (L.it > 64u * 1024u) throw ApiError{MRT_ERR_HIP, "render did not converge"};
       }
-      HIP_CHECK(hipMemcpyAsync(&c->h_status[slot], c->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, st));
-      HIP_CHECK(hipEventRecord(c->ev[slot], st));
-      if (pending) {
-        HIP_CHECK(hipEventSynchronize(c->ev[slot ^ 1]));
-        const Ctrl& s = c->h_status[slot ^ 1];
-        // status after an even number of iterations: the live pool is active[0]
-        if (s.active[0] == 0 && s.next_work >= rp.G) break;
-      }
-      pending = true;
-      slot ^= 1;
-      if (it > 64u * 1024u) throw ApiError{MRT_ERR_HIP, "render did not converge"};
+    }
+    // join: `st` continues after every queue
+    for (int k = 0; k < K; ++k) {
+      HIP_CHECK(hipEventRecord(c->q[k].join, c->q[k].stream));
+      HIP_CHECK(hipStreamWaitEvent(st, c->q[k].join, 0));
     }
     if (timing) {
-      HIP_CHECK(hipStreamSynchronize(st));
+      for (int k = 0; k < K; ++k) HIP_CHECK(hipStreamSynchronize(c->q[k].stream));
       for (auto& m : marks) {
         float t0 = 0, t1 = 0;
         HIP_CHECK(hipEventElapsedTime(&t0, m[0], m[1]));
@@ -1037,9 +1100,6 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
     hipLaunchKernelGGL(k_accumulate, dim3((n_pix + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
                        (const float4*)c->results, n_pix, cs, (const uint32_t*)pl.first, d_rgb, d_b);
     HIP_CHECK(hipGetLastError());
-  }
-  if (count) {
-    // samples/segments for max_depth == 0 are not traced; nothing to add
   }
 }
 
@@ -1070,14 +1130,23 @@ int mrt_create(int device, mrt_ctx** out) {
   c->device = device;
   int rc = guarded(c, [&] {
     HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIP_CHECK(hipMalloc(&c->ctrl, sizeof(Ctrl)));
+    if (const char* e = getenv("MRT_QUEUES")) c->n_queues = std::max(1, std::min(kMaxQueues, atoi(e)));
+    for (int k = 0; k < kMaxQueues; ++k) {
+      Queue& q = c->q[k];
+      HIP_CHECK(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
+      HIP_CHECK(hipMalloc(&q.ctrl, sizeof(Ctrl)));
+      HIP_CHECK(hipHostMalloc(&q.h_status, 2 * sizeof(Ctrl), hipHostMallocDefault));
+      HIP_CHECK(hipHostMalloc(&q.h_work, 2 * sizeof(uint32_t), hipHostMallocDefault));
+      HIP_CHECK(hipEventCreateWithFlags(&q.ev[0], hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&q.ev[1], hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&q.join, hipEventDisableTiming));
+    }
+    HIP_CHECK(hipMalloc(&c->work, 256));
+    HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
     HIP_CHECK(hipMalloc(&c->d_cnt, sizeof(DevCounters)));
     HIP_CHECK(hipMemset(c->d_cnt, 0, sizeof(DevCounters)));
     HIP_CHECK(hipMalloc(&c->dbg, 16));
     HIP_CHECK(hipMemset(c->dbg, 0, 16));
-    HIP_CHECK(hipHostMalloc(&c->h_status, 2 * sizeof(Ctrl), hipHostMallocDefault));
-    HIP_CHECK(hipEventCreateWithFlags(&c->ev[0], hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&c->ev[1], hipEventDisableTiming));
     HIP_CHECK(hipEventCreate(&c->tev[0]));
     HIP_CHECK(hipEventCreate(&c->tev[1]));
     int cus = 0;
@@ -1104,10 +1173,21 @@ int mrt_destroy(mrt_ctx* c) {
   if (!c) return MRT_OK;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  for (Queue& q : c->q)
+    if (q.stream) hipStreamSynchronize(q.stream);
   hipFree(c->scene_mem);
   hipFree(c->pool_mem);
   hipFree(c->results);
-  hipFree(c->ctrl);
+  hipFree(c->work);
+  for (Queue& q : c->q) {
+    hipFree(q.ctrl);
+    if (q.h_status) hipHostFree(q.h_status);
+    if (q.h_work) hipHostFree(q.h_work);
+    for (hipEvent_t e : {q.ev[0], q.ev[1], q.join})
+      if (e) hipEventDestroy(e);
+    if (q.stream) hipStreamDestroy(q.stream);
+  }
+  if (c->fork) hipEventDestroy(c->fork);
   hipFree(c->d_cnt);
   hipFree(c->dbg);
   hipFree(c->d_acc_rgb);
@@ -1116,9 +1196,6 @@ int mrt_destroy(mrt_ctx* c) {
   hipFree(c->d_rhits);
   hipFree(c->slot_ro);
   for (auto& kv : c->pixlists) hipFree(kv.second.first);
-  if (c->h_status) hipHostFree(c->h_status);
-  if (c->ev[0]) hipEventDestroy(c->ev[0]);
-  if (c->ev[1]) hipEventDestroy(c->ev[1]);
   if (c->tev[0]) hipEventDestroy(c->tev[0]);
   if (c->tev[1]) hipEventDestroy(c->tev[1]);
   for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
@@ -1269,15 +1346,17 @@ int mrt_trace_rays(mrt_ctx* c, const float* rays, uint32_t n, float t_min, float
       c->rays_cap = n;
     }
     HIP_CHECK(hipMemcpyAsync(c->d_rays, rays, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
-    ensure_pool(c, n);
+    wait_queues(c, c->stream);
+    ensure_pool(c, (size_t)n * c->n_queues);  // all rays go to queue 0
+    const Queue& q = c->q[0];
     const uint32_t g = (n + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_rays_in, dim3(g), dim3(kBlock), 0, c->stream, (const float*)c->d_rays, n, c->bufs[0]);
+    hipLaunchKernelGGL(k_rays_in, dim3(g), dim3(kBlock), 0, c->stream, (const float*)c->d_rays, n, q.bufs[0]);
     HIP_CHECK(hipGetLastError());
     Ctrl init{{n, 0}, n, 0};
-    HIP_CHECK(hipMemcpyAsync(c->ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, c->stream));
-    launch_trace(c, c->stream, c->bufs[0], 0u, true, t_min, t_max);
+    HIP_CHECK(hipMemcpyAsync(q.ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, c->stream));
+    launch_trace(c, c->stream, q, q.bufs[0], 0u, true, t_min, t_max);
     HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(k_rays_out, dim3(g), dim3(kBlock), 0, c->stream, c->S, c->bufs[0], (const uint4*)c->hits, n,
+    hipLaunchKernelGGL(k_rays_out, dim3(g), dim3(kBlock), 0, c->stream, c->S, q.bufs[0], (const uint4*)q.hits, n,
                        c->d_rhits);
     HIP_CHECK(hipGetLastError());
     std::vector<uint4> h(n);
