@@ -3,14 +3,17 @@
 metric) on BASELINE config 2 — SphereGrid (scenes/sphere_grid.rs, the
 reference's random-spheres scene) at 1920x1080x1024spp, max depth 50.
 
-A step = one pass of the hot path over one batch: `--spp-per-step` samples
-(default 64) of every pixel of the 1920x1080 frame; 16 steps = the full
-1024-spp config. With N GPUs (torchrun, one rank per GPU, RCCL over xGMI)
-each rank renders every N-th 8x8 framebuffer tile of the same frame (strong
-scaling), accumulating its tiles in its own HBM frame, and after every step
-the per-rank frames are summed onto rank 0 with one dist.reduce
+A step = one pass of the hot path over one batch: `--spp-per-step` x N
+samples (default 64 x N) of every pixel of the 1920x1080 frame; at N=1, 16
+steps = the full 1024-spp config. With N GPUs (torchrun, one rank per GPU,
+RCCL over xGMI) each rank renders every N-th 8x8 framebuffer tile of the same
+frame, accumulating its tiles in its own HBM frame, and after every step the
+per-rank frames are summed onto rank 0 with one dist.reduce
 (massrt/shard.py; Image::merge, main.rs:629-638) — bit-identical to the
-1-GPU image; no other exchange exists.
+1-GPU image; no other exchange exists. Each rank's work per step is fixed
+(2.07M/N pixels x 64N spp = 132.7M samples): "weak" scaling — a rank needs
+that much in flight to keep its k_trace launches long compared with their
+tails. `--strong` keeps 64 spp per step for any N instead.
 
 Inputs (scene, BVH, camera) are resident in HBM before timing; the
 accumulation buffers live in HBM. `value` = all samples of all ranks / the
@@ -55,7 +58,8 @@ def parse():
     ap.add_argument("--scene", default="sphere_grid")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp-per-step", type=int, default=64)
+    ap.add_argument("--spp-per-step", type=int, default=64, help="per GPU (x N frame spp per step) unless --strong")
+    ap.add_argument("--strong", action="store_true", help="fixed spp per step for any N (strong scaling)")
     ap.add_argument("--total-spp", type=int, default=1024, help="spp of the config (reporting only)")
     ap.add_argument("--max-depth", type=int, default=50)
     ap.add_argument("--seed", type=int, default=1)
@@ -122,7 +126,8 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-    W, H, spp = a.width, a.height, a.spp_per_step
+    W, H = a.width, a.height
+    spp = a.spp_per_step if a.strong else a.spp_per_step * world
 
     ctx = massrt.Context(torch.cuda.current_device())
     b = massrt.Builder(1).builtin(a.scene, float(massrt.ASPECT_RATIO), str(asset_dir(a.scene)))
@@ -213,7 +218,7 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if (a.strong and world > 1) else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (built-in scene, fixed seeds)",

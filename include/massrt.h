@@ -305,6 +305,27 @@ int mrt_builder_build_bvh(mrt_builder* b); /* World::build_bvh (world.rs:117-122
 /* flatten; pointers stay valid until the builder is freed or modified */
 int mrt_builder_desc(mrt_builder* b, mrt_scene_desc* desc, mrt_camera* camera);
 
+/* ---- display / export (main.rs:640-722, 760-783) ----------------------- */
+/* Image::to_rgb_bytes + dump's row flip: accumulated colour sums (W*H*3
+ * f32) and bounce counts (W*H u32) of `passes` merged 1-spp passes -> RGB8
+ * (W*H*3), TOP row first, exactly the bytes dump() hands to the PNG encoder.
+ * Default: ((sum/passes)^(1/2.2)).min(1).max(0) * 255 as u8 (the gamma byte
+ * is taken from 255 thresholds derived from the host libm powf, so it is the
+ * reference's byte for every input); Depth: (count/passes)/(max/passes).
+ * passes == 0 gives zeros. _device: device pointers on `hip_stream`. */
+#define MRT_DISPLAY_DEFAULT 0u
+#define MRT_DISPLAY_DEPTH 1u
+int mrt_tonemap_device(mrt_ctx* ctx, uint32_t width, uint32_t height, const float* d_accum_rgb,
+                       const uint32_t* d_accum_bounces, uint32_t passes, uint32_t mode, uint8_t* d_rgb8,
+                       void* hip_stream);
+int mrt_tonemap(mrt_ctx* ctx, uint32_t width, uint32_t height, const float* accum_rgb, const uint32_t* accum_bounces,
+                uint32_t passes, uint32_t mode, uint8_t* rgb8);
+/* The 256 Default-mode thresholds (t[k] = f32 bits of the smallest x in
+ * [0, 1] whose byte is >= k), derived from the host libm powf. */
+int mrt_display_gamma_thresholds(uint32_t* out256);
+/* RGB8 (top row first) -> PNG file (8-bit truecolour, zlib). 0 or MRT_ERR_IO. */
+int mrt_write_png(const char* path, uint32_t width, uint32_t height, const uint8_t* rgb8);
+
 /* ---- loaders (host; ply_loader.rs, obj_loader.rs, stl_loader.rs) -------- */
 /* returns triangle count (or -MRT_ERR_IO); out (if non-NULL, capacity cap triangles) gets 9 floats per tri */
 int64_t mrt_load_ply(const char* path, float* out, uint64_t cap);

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../../include/massrt.h"
+#include "../host/display.h"
 #include "path.h"
 #include "upload.h"
 
@@ -568,6 +569,61 @@ __global__ __launch_bounds__(kBlock) void k_selftest_division(unsigned long long
 }
 
 
+// ---- display (main.rs:640-722, 760-767) ----------------------------------
+// Rust f32::min/max (the non-NaN operand wins) and saturating `as u8`.
+__device__ __forceinline__ float rs_min(float a, float b) { return a != a ? b : (b != b ? a : (a < b ? a : b)); }
+__device__ __forceinline__ float rs_max(float a, float b) { return a != a ? b : (b != b ? a : (a > b ? a : b)); }
+__device__ __forceinline__ uint32_t rs_u8(float v) { return !(v > 0.0f) ? 0u : (v >= 255.0f ? 255u : (uint32_t)v); }
+
+// Default-mode byte of x = sum/passes: the count of thresholds <= x for x in
+// [0, 1] (-0.0 counts as 0); NaN or negative x -> NaN.powf -> .min(1.0) = 1.0
+// -> 255; -inf.powf = +inf and x > 1 -> 255.
+// t: host/display.h's table, t[k] = bits of the smallest x in [0,1] whose byte is >= k
+__device__ __forceinline__ uint32_t gamma_byte(const uint32_t* t, float x) {
+  if (!(x >= 0.0f) || x > 1.0f) return 255u;
+  const uint32_t u = __float_as_uint(x) & 0x7FFFFFFFu;  // -0.0 -> powf gives +0 -> byte 0
+  uint32_t lo = 0;  // largest k with t[k] <= u (t[0] = 0 <= u)
+#pragma unroll
+  for (uint32_t step = 128; step > 0; step >>= 1)
+    if (t[lo + step] <= u) lo += step;  // lo + step <= 255
+  return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void k_max_u32(const uint32_t* v, uint32_t n, uint32_t* out) {
+  uint32_t m = 0;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) m = v[i] > m ? v[i] : m;
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t o = __shfl_xor(m, off, 64);
+    m = o > m ? o : m;
+  }
+  if (lane_id() == 0) atomicMax(out, m);
+}
+
+// One thread per pixel; writes the pixel's 3 bytes at the flipped row.
+__global__ __launch_bounds__(kBlock) void k_tonemap(uint32_t W, uint32_t H, const float* rgb, const uint32_t* b,
+                                                    uint32_t passes, uint32_t mode, const uint32_t* max_count,
+                                                    const uint32_t* g, uint8_t* out) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= W * H) return;
+  const uint32_t y = p / W, x = p - y * W;
+  uint8_t* dst = out + ((size_t)(H - 1 - y) * W + x) * 3;
+  if (passes == 0) {
+    dst[0] = dst[1] = dst[2] = 0;
+    return;
+  }
+  const float scale = 1.0f / (float)passes;
+  if (mode == MRT_DISPLAY_DEPTH) {
+    const uint32_t m = *max_count;
+    const float max_depth = (float)(m > 1u ? m : 1u) * scale;
+    const float d = rs_min(rs_max(((float)b[p] * scale) / max_depth, 0.0f), 1.0f);
+    dst[0] = dst[1] = dst[2] = (uint8_t)rs_u8(d * 255.0f);
+  } else {
+    dst[0] = (uint8_t)gamma_byte(g, scale * rgb[3 * (size_t)p]);
+    dst[1] = (uint8_t)gamma_byte(g, scale * rgb[3 * (size_t)p + 1]);
+    dst[2] = (uint8_t)gamma_byte(g, scale * rgb[3 * (size_t)p + 2]);
+  }
+}
+
 // box_hit_any (early decision + exact fallback) against box_hit_exact on
 // rays in the fast domain and boxes whose faces pass within a few ulps of a
 // point of the ray (entry/exit ties), flat boxes, and t_max near the faces.
@@ -673,7 +729,8 @@ struct mrt_ctx {
   void* pool_mem = nullptr;
   Queue q[kMaxQueues];
   int n_queues = 2;            // MRT_QUEUES overrides (1..4)
-  uint32_t* work = nullptr;    // shared work counter of the wavefront loop
+  uint32_t* work = nullptr;    // shared work counter of the wavefront loop (word 1: tonemap max count)
+  uint32_t* gamma_d = nullptr; // display: gamma byte thresholds (256 words)
   hipEvent_t fork = nullptr;
   float4* results = nullptr;
   size_t results_cap = 0;
@@ -1179,6 +1236,7 @@ int mrt_destroy(mrt_ctx* c) {
   hipFree(c->pool_mem);
   hipFree(c->results);
   hipFree(c->work);
+  hipFree(c->gamma_d);
   for (Queue& q : c->q) {
     hipFree(q.ctrl);
     if (q.h_status) hipHostFree(q.h_status);
@@ -1418,6 +1476,55 @@ int mrt_selftest_division(mrt_ctx* c, uint64_t n, uint64_t seed, uint64_t* misma
     HIP_CHECK(hipStreamSynchronize(c->stream));
     HIP_CHECK(hipFree(d));
     *mismatches = h;
+  });
+}
+
+int mrt_tonemap_device(mrt_ctx* c, uint32_t W, uint32_t H, const float* d_rgb, const uint32_t* d_b, uint32_t passes,
+                       uint32_t mode, uint8_t* d_out, void* stream) {
+  return guarded(c, [&] {
+    if (W == 0 || H == 0 || (uint64_t)W * H >= (1ull << 32)) throw ApiError{MRT_ERR_INVALID, "bad image size"};
+    if (mode > MRT_DISPLAY_DEPTH) throw ApiError{MRT_ERR_INVALID, "bad display mode"};
+    if (!d_out || (passes && ((mode == MRT_DISPLAY_DEFAULT && !d_rgb) || (mode == MRT_DISPLAY_DEPTH && !d_b))))
+      throw ApiError{MRT_ERR_INVALID, "null buffer"};
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const uint32_t n = W * H;
+    if (!c->gamma_d) {
+      HIP_CHECK(hipMalloc(&c->gamma_d, 256 * 4));
+      HIP_CHECK(hipMemcpy(c->gamma_d, mrt::gamma_thresholds().data(), 256 * 4, hipMemcpyHostToDevice));
+    }
+    HIP_CHECK(hipMemsetAsync(c->work + 1, 0, 4, st));  // word 1 of the work line: max count
+    if (mode == MRT_DISPLAY_DEPTH && passes) {
+      hipLaunchKernelGGL(k_max_u32, dim3(std::min<uint32_t>((n + kBlock - 1) / kBlock, 4096u)), dim3(kBlock), 0, st,
+                         d_b, n, c->work + 1);
+      HIP_CHECK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_tonemap, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, W, H, d_rgb, d_b, passes,
+                       mode, (const uint32_t*)(c->work + 1), (const uint32_t*)c->gamma_d, d_out);
+    HIP_CHECK(hipGetLastError());
+  });
+}
+
+int mrt_tonemap(mrt_ctx* c, uint32_t W, uint32_t H, const float* rgb, const uint32_t* b, uint32_t passes,
+                uint32_t mode, uint8_t* out) {
+  return guarded(c, [&] {
+    if (W == 0 || H == 0 || (uint64_t)W * H >= (1ull << 32)) throw ApiError{MRT_ERR_INVALID, "bad image size"};
+    if (!out || !rgb || !b) throw ApiError{MRT_ERR_INVALID, "null buffer"};
+    const size_t n = (size_t)W * H;
+    void* mem = nullptr;
+    HIP_CHECK(hipMalloc(&mem, n * 12 + n * 4 + n * 3 + 256));
+    float* d_rgb = (float*)mem;
+    uint32_t* d_b = (uint32_t*)(d_rgb + 3 * n);
+    uint8_t* d_out = (uint8_t*)(d_b + n);
+    HIP_CHECK(hipMemcpyAsync(d_rgb, rgb, n * 12, hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(hipMemcpyAsync(d_b, b, n * 4, hipMemcpyHostToDevice, c->stream));
+    int rc = mrt_tonemap_device(c, W, H, d_rgb, d_b, passes, mode, d_out, c->stream);
+    if (rc != MRT_OK) {
+      hipFree(mem);
+      throw ApiError{rc, c->err};
+    }
+    HIP_CHECK(hipMemcpyAsync(out, d_out, n * 3, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    HIP_CHECK(hipFree(mem));
   });
 }
 

@@ -4,6 +4,7 @@
 // reference-topology tree to the device half as an mrt_scene_desc.
 #include <string.h>
 
+#include "display.h"
 #include "world.h"
 
 using namespace massrt;
@@ -258,6 +259,22 @@ static int64_t copy_tris(const std::vector<std::array<V3, 3>>& f, float* out, ui
       }
   }
   return (int64_t)f.size();
+}
+
+int mrt_display_gamma_thresholds(uint32_t* out256) {
+  if (!out256) return MRT_ERR_INVALID;
+  const auto& t = mrt::gamma_thresholds();
+  for (int k = 0; k < 256; ++k) out256[k] = t[k];
+  return MRT_OK;
+}
+
+int mrt_write_png(const char* path, uint32_t width, uint32_t height, const uint8_t* rgb8) {
+  std::string err;
+  if (!path || !mrt::write_png_rgb8(path, width, height, rgb8, err)) {
+    g_builder_error = path ? err : "null path";
+    return MRT_ERR_IO;
+  }
+  return MRT_OK;
 }
 
 int64_t mrt_load_ply(const char* path, float* out, uint64_t cap) {

@@ -161,6 +161,7 @@ EXPORTED_SYMBOLS = [
     "mrt_builder_add_sphere", "mrt_builder_add_triangle", "mrt_builder_model", "mrt_builder_model_from_ply",
     "mrt_builder_add_instance", "mrt_builder_camera", "mrt_builder_build_bvh", "mrt_builder_desc",
     "mrt_builder_last_error", "mrt_load_ply", "mrt_load_stl", "mrt_load_obj",
+    "mrt_tonemap_device", "mrt_tonemap", "mrt_write_png", "mrt_display_gamma_thresholds",
 ]
 
 _lib = None
@@ -217,6 +218,10 @@ def lib() -> C.CDLL:
         "mrt_load_ply": (I64, [C.c_char_p, fp, U64]),
         "mrt_load_stl": (I64, [C.c_char_p, fp, U64]),
         "mrt_load_obj": (I64, [C.c_char_p, fp, U64]),
+        "mrt_tonemap_device": (I, [P, U32, U32, P, P, U32, U32, P, P]),
+        "mrt_tonemap": (I, [P, U32, U32, fp, C.POINTER(C.c_uint32), U32, U32, C.POINTER(C.c_uint8)]),
+        "mrt_write_png": (I, [C.c_char_p, U32, U32, C.POINTER(C.c_uint8)]),
+        "mrt_display_gamma_thresholds": (I, [C.POINTER(C.c_uint32)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -458,6 +463,20 @@ class Context:
         self._check(lib().mrt_selftest_division(self.h, n, seed, C.byref(m)))
         return int(m.value)
 
+    def tonemap(self, width, height, rgb, bounces, passes, mode=0) -> np.ndarray:
+        """Image::to_rgb_bytes + dump's row flip on the GPU: (H, W, 3) uint8, top row first."""
+        rgb = np.ascontiguousarray(rgb, dtype=np.float32).reshape(-1)
+        b = np.ascontiguousarray(bounces, dtype=np.uint32).reshape(-1)
+        out = np.empty(width * height * 3, dtype=np.uint8)
+        self._check(lib().mrt_tonemap(self.h, width, height, _fptr(rgb), b.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                      passes, mode, out.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return out.reshape(height, width, 3)
+
+    def tonemap_device(self, width, height, d_rgb: int, d_bounces: int, passes: int, mode: int, d_out: int,
+                       stream: int | None = None):
+        self._check(lib().mrt_tonemap_device(self.h, width, height, C.c_void_p(d_rgb), C.c_void_p(d_bounces), passes,
+                                             mode, C.c_void_p(d_out), C.c_void_p(stream or 0)))
+
     def selftest_slab(self, n: int, seed: int = 1):
         """(mismatches, near_ties) of the early slab decision vs the exact test."""
         m, t = C.c_uint64(), C.c_uint64()
@@ -471,6 +490,23 @@ class Context:
 
     def reset_kernel_stats(self):
         self._check(lib().mrt_reset_kernel_stats(self.h))
+
+
+DISPLAY_DEFAULT, DISPLAY_DEPTH = 0, 1
+
+
+def gamma_thresholds() -> np.ndarray:
+    t = np.zeros(256, dtype=np.uint32)
+    lib().mrt_display_gamma_thresholds(t.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return t
+
+
+def write_png(path, rgb8: np.ndarray):
+    """RGB8 (H, W, 3), top row first -> PNG (host code in libmassrt)."""
+    a = np.ascontiguousarray(rgb8, dtype=np.uint8)
+    h, w = a.shape[0], a.shape[1]
+    if lib().mrt_write_png(str(path).encode(), w, h, a.ctypes.data_as(C.POINTER(C.c_uint8))) != 0:
+        raise MassrtError(lib().mrt_builder_last_error().decode())
 
 
 def load_ply(path) -> np.ndarray:

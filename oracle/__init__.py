@@ -65,6 +65,8 @@ def lib() -> C.CDLL:
         "orc_path_rng": (None, [U64, U32, U32, U32, C.POINTER(C.c_uint64), fp]),
         "orc_reset_counters": (None, [P]),
         "orc_set_counting": (None, [P, I]),
+        "orc_tonemap": (I, [U32, U32, fp, up, U32, U32, C.POINTER(C.c_uint8)]),
+        "orc_tonemap_check": (U64, [up, I]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -92,6 +94,22 @@ def _up(a):
 
 def _f3(v):
     return np.ascontiguousarray(np.asarray(v, dtype=np.float32).reshape(3))
+
+
+def tonemap(width, height, rgb, bounces, passes, mode=0) -> np.ndarray:
+    """Image::to_rgb_bytes + dump row flip (main.rs:640-722,760-767) on the CPU."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32).reshape(-1)
+    b = np.ascontiguousarray(bounces, dtype=np.uint32).reshape(-1)
+    out = np.empty(width * height * 3, dtype=np.uint8)
+    lib().orc_tonemap(width, height, _fp(rgb), _up(b), passes, mode, out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return out.reshape(height, width, 3)
+
+
+def tonemap_check(threads=0):
+    """(mismatches, thresholds): the threshold-table byte vs powf over every f32 in [0, 1]."""
+    t = np.zeros(256, dtype=np.uint32)
+    bad = lib().orc_tonemap_check(_up(t), threads)
+    return int(bad), t
 
 
 def wyrand(seed: int, n: int):

@@ -1530,6 +1530,91 @@ void orc_path_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, ui
   for (uint32_t i = 0; i < n; ++i) out_u64[i] = a.next(), out_f32[i] = b.f32();
 }
 
+// ---- tonemap / export (main.rs:640-722, 760-783) ------------------------
+// Rust: ((scale * f).powf(1.0 / 2.2).min(1.0).max(0.0) * 255.0) as u8, where
+// f32::min/max return the non-NaN operand and `as u8` saturates (NaN -> 0).
+static uint8_t rust_u8(float v) {
+  if (!(v == v)) return 0;
+  if (v <= 0.0f) return 0;
+  if (v >= 255.0f) return 255;
+  return (uint8_t)v;  // truncation toward zero
+}
+static float rust_min(float a, float b) { return a != a ? b : (b != b ? a : (a < b ? a : b)); }
+static float rust_max(float a, float b) { return a != a ? b : (b != b ? a : (a > b ? a : b)); }
+static uint8_t gamma_byte(float x) {
+  const float g = 1.0f / 2.2f;
+  float v = rust_max(rust_min(powf(x, g), 1.0f), 0.0f);
+  return rust_u8(v * 255.0f);
+}
+
+int orc_tonemap(uint32_t W, uint32_t H, const float* rgb, const uint32_t* b, uint32_t passes, uint32_t mode,
+                uint8_t* out) {
+  const size_t n = (size_t)W * H;
+  if (passes == 0) {
+    memset(out, 0, n * 3);
+    return 0;
+  }
+  const float scale = 1.0f / (float)passes;
+  float max_depth = 0.0f;
+  if (mode == 1) {
+    uint32_t m = 0;
+    for (size_t i = 0; i < n; ++i) m = b[i] > m ? b[i] : m;
+    max_depth = (float)(m > 1 ? m : 1) * scale;
+  }
+  for (uint32_t y = 0; y < H; ++y)
+    for (uint32_t x = 0; x < W; ++x) {
+      const size_t src = (size_t)y * W + x;
+      uint8_t* dst = out + ((size_t)(H - 1 - y) * W + x) * 3;  // dump(): rows reversed
+      if (mode == 1) {
+        float d = rust_min(rust_max(((float)b[src] * scale) / max_depth, 0.0f), 1.0f);
+        dst[0] = dst[1] = dst[2] = rust_u8(d * 255.0f);
+      } else {
+        for (int c = 0; c < 3; ++c) dst[c] = gamma_byte(scale * rgb[src * 3 + c]);
+      }
+    }
+  return 0;
+}
+
+uint64_t orc_tonemap_check(uint32_t* thr, int threads) {
+  // thresholds by bisection on the (non-negative) float bit patterns
+  thr[0] = 0;
+  for (int k = 1; k < 256; ++k) {
+    uint32_t lo = 0, hi = 0x3F800000u;  // gamma_byte(1.0) == 255
+    while (lo < hi) {
+      uint32_t mid = lo + (hi - lo) / 2;
+      float x;
+      memcpy(&x, &mid, 4);
+      if (gamma_byte(x) >= k) hi = mid; else lo = mid + 1;
+    }
+    thr[k] = lo;
+  }
+  if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  std::atomic<uint64_t> bad{0};
+  std::vector<std::thread> ts;
+  const uint32_t end = 0x3F800001u;
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&, t] {
+      uint64_t local = 0;
+      const uint32_t per = (end + threads - 1) / threads;
+      const uint32_t a = per * t, z = std::min<uint64_t>((uint64_t)per * (t + 1), end);
+      int k = 0;
+      for (uint32_t u = a; u < z; ++u) {
+        float x;
+        memcpy(&x, &u, 4);
+        if (u == a) {
+          k = 0;
+          while (k < 255 && thr[k + 1] <= u) ++k;
+        } else {
+          while (k < 255 && thr[k + 1] <= u) ++k;
+        }
+        local += gamma_byte(x) != k;
+      }
+      bad += local;
+    });
+  for (auto& th : ts) th.join();
+  return bad.load();
+}
+
 void orc_get_counters(orc_scene* s, orc_counters* o) {
   const Counters& c = s->counters;
   *o = orc_counters{c.samples,        c.segments,      c.node_visits,  c.sphere_tests, c.triangle_tests, c.instance_entries,

@@ -86,6 +86,16 @@ double orc_bench_reference_mode(orc_scene* s, uint32_t W, uint32_t H, uint32_t p
                                 uint32_t row_begin, uint32_t row_end);
 void orc_wyrand(uint64_t seed, uint32_t n, uint64_t* out_u64, float* out_f32);
 void orc_path_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint64_t* out_u64, float* out_f32);
+// Image::to_rgb_bytes (main.rs:640-722) + dump's row flip (main.rs:760-767):
+// accumulated colour sums and bounce counts of `passes` merged passes ->
+// RGB8, top row first. mode 0 Default (gamma 1/2.2), 1 Depth.
+int orc_tonemap(uint32_t W, uint32_t H, const float* accum_rgb, const uint32_t* accum_bounces, uint32_t passes,
+                uint32_t mode, uint8_t* out_rgb8);
+// Exhaustive check of the byte a Default-mode component takes, over every
+// f32 in [0, 1] (bit patterns 0..0x3F800000): returns the number of x whose
+// byte differs from the count of thresholds <= x in `thresholds[1..255]`
+// (the device's method) and writes the thresholds it derived (256 words).
+uint64_t orc_tonemap_check(uint32_t* thresholds, int threads);
 void orc_get_counters(orc_scene* s, orc_counters* out);
 void orc_reset_counters(orc_scene* s);
 void orc_set_counting(orc_scene* s, int on);

@@ -319,3 +319,33 @@ def test_slab_early_decision_matches_exact(ctx):
         bad, ties = ctx.selftest_slab(1 << 26, seed=seed)
         assert bad == 0
         assert ties > 100_000  # the near-tie fallback is exercised
+
+
+def test_tonemap_matches_oracle_bytes(ctx, small_scenes, tmp_path):
+    """Image::to_rgb_bytes + dump row flip (main.rs:640-722,760-767) on the GPU:
+    byte-exact against the CPU restatement, for a render and for accumulations
+    with every edge the formula has (0, >1, NaN, negative, inf, tiny)."""
+    b, o = small_scenes["cornell"]
+    ctx.upload(b)
+    W, H, spp = 48, 27, 3
+    rgb, bo = ctx.render(W, H, 0, spp, seed=4)
+    for mode in (massrt.DISPLAY_DEFAULT, massrt.DISPLAY_DEPTH):
+        for passes in (spp, 0, 1):
+            got = ctx.tonemap(W, H, rgb, bo, passes, mode)
+            exp = oracle.tonemap(W, H, rgb, bo, passes, mode)
+            assert np.array_equal(got, exp), (mode, passes, int((got != exp).sum()))
+    rng = np.random.default_rng(11)
+    W2, H2 = 257, 129
+    x = rng.random(W2 * H2 * 3, dtype=np.float32) * np.float32(3.0)
+    specials = np.array([0.0, 1.0, 3.0, np.nan, -1.0, -0.0, np.inf, -np.inf, 1e-38, 1e-45, 2.9999998], np.float32)
+    x[: specials.size] = specials
+    # values at the gamma thresholds and one ulp either side (x3 passes scaling undone)
+    t = massrt.gamma_thresholds()[1:].astype(np.int64)
+    edge = np.concatenate([t - 1, t, t + 1]).astype(np.uint32).view(np.float32) * np.float32(3.0)
+    x[100:100 + edge.size] = edge
+    bb = rng.integers(0, 60, size=W2 * H2, dtype=np.uint32)
+    for mode in (massrt.DISPLAY_DEFAULT, massrt.DISPLAY_DEPTH):
+        got = ctx.tonemap(W2, H2, x, bb, 3, mode)
+        exp = oracle.tonemap(W2, H2, x, bb, 3, mode)
+        assert np.array_equal(got, exp), (mode, int((got != exp).sum()))
+    massrt.write_png(tmp_path / "cornell.png", ctx.tonemap(W, H, rgb, bo, spp))
