@@ -226,7 +226,8 @@ def main():
                 "workload": f"{a.scene} {W}x{H}x{a.total_spp}spp, max_depth {a.max_depth}",
                 "scene": a.scene, "width": W, "height": H, "spp_per_step": spp,
                 "samples_per_step": W * H * spp, "max_depth": a.max_depth,
-                "parallelism": f"tile-shard x{world}" + (" + RCCL reduce" if world > 1 else ""),
+                "parallelism": f"tile-shard x{world}" + (
+                    (" + RCCL reduce" if a.dist_backend == "nccl" else f" + {a.dist_backend} reduce") if world > 1 else ""),
                 "mean_bounces_per_sample": round(mean_bounces, 4),
                 "mrays_per_s": round(value * (roof["segments_per_sample"] if roof else float("nan")), 1),
             },
