@@ -315,11 +315,23 @@ int mrt_builder_desc(mrt_builder* b, mrt_scene_desc* desc, mrt_camera* camera);
  * passes == 0 gives zeros. _device: device pointers on `hip_stream`. */
 #define MRT_DISPLAY_DEFAULT 0u
 #define MRT_DISPLAY_DEPTH 1u
+#define MRT_DISPLAY_ALBEDO 2u /* accum_rgb = the pre-pass albedo; p.min(1).max(0).powf(1/2.2) (passes ignored) */
+#define MRT_DISPLAY_NORMAL 3u /* accum_rgb = the pre-pass normal; (p + 1) / 2 (passes ignored) */
 int mrt_tonemap_device(mrt_ctx* ctx, uint32_t width, uint32_t height, const float* d_accum_rgb,
                        const uint32_t* d_accum_bounces, uint32_t passes, uint32_t mode, uint8_t* d_rgb8,
                        void* hip_stream);
 int mrt_tonemap(mrt_ctx* ctx, uint32_t width, uint32_t height, const float* accum_rgb, const uint32_t* accum_bounces,
                 uint32_t passes, uint32_t mode, uint8_t* rgb8);
+/* Camera::albedo_normal pre-pass (world.rs:81-92, main.rs:181-222): one ray
+ * per pixel through (x/(W-1), y/(H-1)), no jitter; albedo = the scatter
+ * attenuation (emission if the material absorbs, background on a miss),
+ * normal = the hit's face-oriented world normal (0 on a miss). W*H*3 f32
+ * each, row y = pixel row y (FloatBuffer, main.rs:544-575). The reference
+ * draws this pass from thread-local RNG; here pixel p uses the path stream
+ * keyed (seed, p, sample 0xFFFFFFFF). _device: device pointers on `hip_stream`. */
+int mrt_prepass_device(mrt_ctx* ctx, uint32_t width, uint32_t height, uint64_t seed, float* d_albedo, float* d_normal,
+                       void* hip_stream);
+int mrt_prepass(mrt_ctx* ctx, uint32_t width, uint32_t height, uint64_t seed, float* albedo, float* normal);
 /* The 256 Default-mode thresholds (t[k] = f32 bits of the smallest x in
  * [0, 1] whose byte is >= k), derived from the host libm powf. */
 int mrt_display_gamma_thresholds(uint32_t* out256);

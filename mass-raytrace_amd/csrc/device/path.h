@@ -604,14 +604,20 @@ struct DevCamera {
 };
 
 // main.rs:258-260 + Camera::ray (world.rs:53-63)
-MRT_DEV void camera_ray(const DevCamera& cam, uint32_t x, uint32_t y, uint32_t W, uint32_t H, PathRng& rng, V3& o,
-                        V3& d) {
-  float u = ((float)x + rng.f32()) / (float)(W - 1);
-  float v = ((float)y + rng.f32()) / (float)(H - 1);
+// Camera::ray (world.rs:53-63) through (u, v)
+MRT_DEV void camera_ray_uv(const DevCamera& cam, float u, float v, PathRng& rng, V3& o, V3& d) {
   V3 blur = random_in_unit_disk(rng) * cam.lens_radius;
   V3 offset = cam.u * blur.x + cam.v * blur.y;
   o = cam.origin + offset;
   d = (((cam.llc + (cam.horizontal * u)) + (cam.vertical * v)) - cam.origin) - offset;
+}
+
+// the jittered sample ray of pixel (x, y) (main.rs:258-260)
+MRT_DEV void camera_ray(const DevCamera& cam, uint32_t x, uint32_t y, uint32_t W, uint32_t H, PathRng& rng, V3& o,
+                        V3& d) {
+  float u = ((float)x + rng.f32()) / (float)(W - 1);
+  float v = ((float)y + rng.f32()) / (float)(H - 1);
+  camera_ray_uv(cam, u, v, rng, o, d);
 }
 
 MRT_DEV V3 background(const DevScene& S, V3 d, LocalCounters& lc) {

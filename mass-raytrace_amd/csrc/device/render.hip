@@ -599,6 +599,35 @@ __global__ __launch_bounds__(kBlock) void k_max_u32(const uint32_t* v, uint32_t 
   if (lane_id() == 0) atomicMax(out, m);
 }
 
+// Camera::albedo_normal for pixel p (one ray, no jitter). The rays go through
+// ray_ro/ray_rd so that the traversal can re-read them (TravIn).
+__global__ __launch_bounds__(kBlock) void k_prepass(DevScene S, DevCamera cam, uint32_t W, uint32_t H,
+                                                    unsigned long long seed, float4* ray_ro, float4* ray_rd,
+                                                    float* albedo, float* normal) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= W * H) return;
+  const uint32_t y = p / W, x = p - y * W;
+  PathRng rng = path_rng(seed, p, 0xFFFFFFFFu);
+  V3 o, d;
+  camera_ray_uv(cam, (float)x / (float)(W - 1), (float)y / (float)(H - 1), rng, o, d);
+  ray_ro[p] = make_float4(o.x, o.y, o.z, 0.0f);
+  ray_rd[p] = make_float4(d.x, d.y, d.z, 0.0f);
+  const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), ray_ro, ray_rd, kTmin};
+  LocalCounters lc;
+  const Hit h = closest_hit<false>(tin, p, INFINITY, lc);
+  V3 a{0.0f, 0.0f, 0.0f}, n{0.0f, 0.0f, 0.0f};
+  if (h.prim != kRefNone) {
+    Surf s = resolve_hit(S, o, d, h);
+    V3 emitted, atten, nd;
+    a = scatter(S, s, d, rng, emitted, atten, nd, lc) ? atten : emitted;
+    n = s.normal;
+  } else {
+    a = background(S, d, lc);
+  }
+  albedo[3 * (size_t)p] = a.x, albedo[3 * (size_t)p + 1] = a.y, albedo[3 * (size_t)p + 2] = a.z;
+  normal[3 * (size_t)p] = n.x, normal[3 * (size_t)p + 1] = n.y, normal[3 * (size_t)p + 2] = n.z;
+}
+
 // One thread per pixel; writes the pixel's 3 bytes at the flipped row.
 __global__ __launch_bounds__(kBlock) void k_tonemap(uint32_t W, uint32_t H, const float* rgb, const uint32_t* b,
                                                     uint32_t passes, uint32_t mode, const uint32_t* max_count,
@@ -607,6 +636,19 @@ __global__ __launch_bounds__(kBlock) void k_tonemap(uint32_t W, uint32_t H, cons
   if (p >= W * H) return;
   const uint32_t y = p / W, x = p - y * W;
   uint8_t* dst = out + ((size_t)(H - 1 - y) * W + x) * 3;
+  if (mode == MRT_DISPLAY_ALBEDO || mode == MRT_DISPLAY_NORMAL) {  // main.rs:689-718
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v = rgb[3 * (size_t)p + c];
+      if (mode == MRT_DISPLAY_NORMAL) {
+        dst[c] = (uint8_t)rs_u8(((v + 1.0f) / 2.0f) * 255.0f);
+      } else {  // p.min(1).max(0).powf(1/2.2): NaN -> 1 -> 255, <= 0 -> 0
+        const float q = rs_max(rs_min(v, 1.0f), 0.0f);
+        dst[c] = (uint8_t)(q >= 1.0f ? 255u : gamma_byte(g, q));
+      }
+    }
+    return;
+  }
   if (passes == 0) {
     dst[0] = dst[1] = dst[2] = 0;
     return;
@@ -1483,8 +1525,10 @@ int mrt_tonemap_device(mrt_ctx* c, uint32_t W, uint32_t H, const float* d_rgb, c
                        uint32_t mode, uint8_t* d_out, void* stream) {
   return guarded(c, [&] {
     if (W == 0 || H == 0 || (uint64_t)W * H >= (1ull << 32)) throw ApiError{MRT_ERR_INVALID, "bad image size"};
-    if (mode > MRT_DISPLAY_DEPTH) throw ApiError{MRT_ERR_INVALID, "bad display mode"};
-    if (!d_out || (passes && ((mode == MRT_DISPLAY_DEFAULT && !d_rgb) || (mode == MRT_DISPLAY_DEPTH && !d_b))))
+    if (mode > MRT_DISPLAY_NORMAL) throw ApiError{MRT_ERR_INVALID, "bad display mode"};
+    const bool aux = mode == MRT_DISPLAY_ALBEDO || mode == MRT_DISPLAY_NORMAL;
+    if (!d_out || (aux && !d_rgb) ||
+        (passes && ((mode == MRT_DISPLAY_DEFAULT && !d_rgb) || (mode == MRT_DISPLAY_DEPTH && !d_b))))
       throw ApiError{MRT_ERR_INVALID, "null buffer"};
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     const uint32_t n = W * H;
@@ -1525,6 +1569,42 @@ int mrt_tonemap(mrt_ctx* c, uint32_t W, uint32_t H, const float* rgb, const uint
     HIP_CHECK(hipMemcpyAsync(out, d_out, n * 3, hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(hipStreamSynchronize(c->stream));
     HIP_CHECK(hipFree(mem));
+  });
+}
+
+int mrt_prepass_device(mrt_ctx* c, uint32_t W, uint32_t H, uint64_t seed, float* d_albedo, float* d_normal,
+                       void* stream) {
+  return guarded(c, [&] {
+    if (!c->has_scene) throw ApiError{MRT_ERR_STATE, "no scene uploaded"};
+    if (!c->has_camera) throw ApiError{MRT_ERR_STATE, "no camera set"};
+    if (W == 0 || H == 0 || (uint64_t)W * H >= (1ull << 32)) throw ApiError{MRT_ERR_INVALID, "bad image size"};
+    if (!d_albedo || !d_normal) throw ApiError{MRT_ERR_INVALID, "null buffer"};
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    wait_queues(c, st);
+    const uint32_t n = W * H;
+    ensure_slots(c, n);  // the pre-pass rays
+    hipLaunchKernelGGL(k_prepass, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c->S, c->cam, W, H,
+                       (unsigned long long)seed, c->slot_ro, c->slot_rd, d_albedo, d_normal);
+    HIP_CHECK(hipGetLastError());
+  });
+}
+
+int mrt_prepass(mrt_ctx* c, uint32_t W, uint32_t H, uint64_t seed, float* albedo, float* normal) {
+  return guarded(c, [&] {
+    if (W == 0 || H == 0 || (uint64_t)W * H >= (1ull << 32)) throw ApiError{MRT_ERR_INVALID, "bad image size"};
+    if (!albedo || !normal) throw ApiError{MRT_ERR_INVALID, "null buffer"};
+    const size_t n = (size_t)W * H;
+    float* d = nullptr;
+    HIP_CHECK(hipMalloc(&d, n * 24));
+    int rc = mrt_prepass_device(c, W, H, seed, d, d + 3 * n, c->stream);
+    if (rc != MRT_OK) {
+      hipFree(d);
+      throw ApiError{rc, c->err};
+    }
+    HIP_CHECK(hipMemcpyAsync(albedo, d, n * 12, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipMemcpyAsync(normal, d + 3 * n, n * 12, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    HIP_CHECK(hipFree(d));
   });
 }
 

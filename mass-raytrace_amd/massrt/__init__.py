@@ -162,6 +162,7 @@ EXPORTED_SYMBOLS = [
     "mrt_builder_add_instance", "mrt_builder_camera", "mrt_builder_build_bvh", "mrt_builder_desc",
     "mrt_builder_last_error", "mrt_load_ply", "mrt_load_stl", "mrt_load_obj",
     "mrt_tonemap_device", "mrt_tonemap", "mrt_write_png", "mrt_display_gamma_thresholds",
+    "mrt_prepass_device", "mrt_prepass",
 ]
 
 _lib = None
@@ -222,6 +223,8 @@ def lib() -> C.CDLL:
         "mrt_tonemap": (I, [P, U32, U32, fp, C.POINTER(C.c_uint32), U32, U32, C.POINTER(C.c_uint8)]),
         "mrt_write_png": (I, [C.c_char_p, U32, U32, C.POINTER(C.c_uint8)]),
         "mrt_display_gamma_thresholds": (I, [C.POINTER(C.c_uint32)]),
+        "mrt_prepass_device": (I, [P, U32, U32, U64, P, P, P]),
+        "mrt_prepass": (I, [P, U32, U32, U64, fp, fp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -472,6 +475,13 @@ class Context:
                                       passes, mode, out.ctypes.data_as(C.POINTER(C.c_uint8))))
         return out.reshape(height, width, 3)
 
+    def prepass(self, width, height, seed=1):
+        """Camera::albedo_normal pre-pass: (albedo, normal) float32 [H*W*3] each."""
+        a = np.empty(width * height * 3, dtype=np.float32)
+        n = np.empty(width * height * 3, dtype=np.float32)
+        self._check(lib().mrt_prepass(self.h, width, height, seed, _fptr(a), _fptr(n)))
+        return a, n
+
     def tonemap_device(self, width, height, d_rgb: int, d_bounces: int, passes: int, mode: int, d_out: int,
                        stream: int | None = None):
         self._check(lib().mrt_tonemap_device(self.h, width, height, C.c_void_p(d_rgb), C.c_void_p(d_bounces), passes,
@@ -492,7 +502,7 @@ class Context:
         self._check(lib().mrt_reset_kernel_stats(self.h))
 
 
-DISPLAY_DEFAULT, DISPLAY_DEPTH = 0, 1
+DISPLAY_DEFAULT, DISPLAY_DEPTH, DISPLAY_ALBEDO, DISPLAY_NORMAL = 0, 1, 2, 3
 
 
 def gamma_thresholds() -> np.ndarray:

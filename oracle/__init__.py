@@ -67,6 +67,7 @@ def lib() -> C.CDLL:
         "orc_set_counting": (None, [P, I]),
         "orc_tonemap": (I, [U32, U32, fp, up, U32, U32, C.POINTER(C.c_uint8)]),
         "orc_tonemap_check": (U64, [up, I]),
+        "orc_prepass": (I, [P, U32, U32, U64, I, fp, fp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -238,6 +239,13 @@ class Scene:
         self._chk(lib().orc_render(self.h, width, height, spp_begin, spp_count, seed, max_depth, shard_index,
                                    shard_count, threads, _fp(rgb), _up(b)))
         return rgb, b
+
+    def prepass(self, width, height, seed=1, threads=0):
+        """Camera::albedo_normal pre-pass (world.rs:81-92): (albedo, normal) float32 [H*W*3]."""
+        a = np.zeros(width * height * 3, dtype=np.float32)
+        n = np.zeros(width * height * 3, dtype=np.float32)
+        self._chk(lib().orc_prepass(self.h, width, height, seed, threads, _fp(a), _fp(n)))
+        return a, n
 
     def render_pixels(self, width, height, pixels, spp_begin=0, spp_count=1, seed=1, max_depth=50, threads=0):
         px = np.ascontiguousarray(pixels, dtype=np.uint32)

@@ -1550,6 +1550,17 @@ static uint8_t gamma_byte(float x) {
 int orc_tonemap(uint32_t W, uint32_t H, const float* rgb, const uint32_t* b, uint32_t passes, uint32_t mode,
                 uint8_t* out) {
   const size_t n = (size_t)W * H;
+  if (mode == 2 || mode == 3) {  // Albedo / Normal views of the pre-pass buffers (main.rs:689-718)
+    const float g = 1.0f / 2.2f;
+    for (uint32_t y = 0; y < H; ++y)
+      for (uint32_t x = 0; x < W; ++x)
+        for (int c = 0; c < 3; ++c) {
+          const float p = rgb[((size_t)y * W + x) * 3 + c];
+          const float v = mode == 2 ? powf(rust_max(rust_min(p, 1.0f), 0.0f), g) : (p + 1.0f) / 2.0f;
+          out[((size_t)(H - 1 - y) * W + x) * 3 + c] = rust_u8(v * 255.0f);
+        }
+    return 0;
+  }
   if (passes == 0) {
     memset(out, 0, n * 3);
     return 0;
@@ -1573,6 +1584,42 @@ int orc_tonemap(uint32_t W, uint32_t H, const float* rgb, const uint32_t* b, uin
       }
     }
   return 0;
+}
+
+int orc_prepass(orc_scene* s, uint32_t W, uint32_t H, uint64_t seed, int threads, float* albedo, float* normal) {
+  return guard([&] {
+    std::exception_ptr err;
+    run_threads(threads, W * H, [&](uint32_t b, uint32_t e) {
+      Ctx c;
+      try {
+        for (uint32_t p = b; p < e; ++p) {
+          const uint32_t x = p % W, y = p / W;
+          PathRng rng(seed, p, 0xFFFFFFFFu);
+          c.rng = &rng;
+          const float u = (float)x / (float)(W - 1), v = (float)y / (float)(H - 1);
+          const Ray ray = s->camera.ray(u, v, c);
+          V3 a{0, 0, 0}, n{0, 0, 0};
+          Hit hit;
+          if (s->world.intersect(ray, 0.001f, INFINITY, hit, c)) {
+            V3 emitted{0, 0, 0};
+            hit.material->emit(hit, emitted);
+            Scatter sc;
+            a = hit.material->scatter(ray, hit, c, sc) ? sc.attenuation : emitted;
+            n = hit.normal;
+          } else {
+            a = s->world.background->background(ray, c);
+          }
+          albedo[3 * (size_t)p] = a.x, albedo[3 * (size_t)p + 1] = a.y, albedo[3 * (size_t)p + 2] = a.z;
+          normal[3 * (size_t)p] = n.x, normal[3 * (size_t)p + 1] = n.y, normal[3 * (size_t)p + 2] = n.z;
+        }
+      } catch (...) {
+        std::lock_guard<std::mutex> gl(s->mu);
+        err = std::current_exception();
+      }
+    });
+    if (err) std::rethrow_exception(err);
+    return 0;
+  });
 }
 
 uint64_t orc_tonemap_check(uint32_t* thr, int threads) {

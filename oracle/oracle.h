@@ -88,9 +88,14 @@ void orc_wyrand(uint64_t seed, uint32_t n, uint64_t* out_u64, float* out_f32);
 void orc_path_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint64_t* out_u64, float* out_f32);
 // Image::to_rgb_bytes (main.rs:640-722) + dump's row flip (main.rs:760-767):
 // accumulated colour sums and bounce counts of `passes` merged passes ->
-// RGB8, top row first. mode 0 Default (gamma 1/2.2), 1 Depth.
+// RGB8, top row first. mode 0 Default (gamma 1/2.2), 1 Depth, 2 Albedo and
+// 3 Normal (accum_rgb = the pre-pass buffer; passes ignored).
 int orc_tonemap(uint32_t W, uint32_t H, const float* accum_rgb, const uint32_t* accum_bounces, uint32_t passes,
                 uint32_t mode, uint8_t* out_rgb8);
+// Camera::albedo_normal pre-pass (world.rs:81-92, main.rs:181-222): one ray per
+// pixel through (x/(W-1), y/(H-1)); albedo/normal W*H*3 (row y = pixel row y).
+// Per-pixel RNG: the path stream keyed (seed, pixel, 0xFFFFFFFF).
+int orc_prepass(orc_scene* s, uint32_t W, uint32_t H, uint64_t seed, int threads, float* albedo, float* normal);
 // Exhaustive check of the byte a Default-mode component takes, over every
 // f32 in [0, 1] (bit patterns 0..0x3F800000): returns the number of x whose
 // byte differs from the count of thresholds <= x in `thresholds[1..255]`

@@ -50,3 +50,30 @@ def test_write_png_roundtrip(tmp_path):
     assert np.array_equal(back, img)
     with pytest.raises(massrt.MassrtError):
         massrt.write_png(tmp_path / "no" / "such" / "dir.png", img)
+
+
+def test_oracle_prepass_furnace_and_views(golden_dir):
+    """Camera::albedo_normal (world.rs:81-92): a Lambertian sphere's albedo is
+    its colour, misses give the background and a zero normal; the Albedo and
+    Normal views follow main.rs:689-718."""
+    o = oracle.Scene(3)
+    o.background(massrt.BG_SOLID, 0, (0.25, 0.5, 0.75))
+    m = o.material(massrt.MAT_LAMBERTIAN, o.solid(0.8, 0.4, 0.2, 1.0))
+    o.add_sphere(m, (0, 0, 0), 1.0)
+    o.build_bvh()
+    o.camera(40.0, (0, 0, 4), (0, 0, 0), aspect=1.0)
+    W = H = 33
+    a, n = o.prepass(W, H, seed=5)
+    a, n = a.reshape(H, W, 3), n.reshape(H, W, 3)
+    hit = np.linalg.norm(n, axis=2) > 0
+    assert hit[H // 2, W // 2] and not hit[0, 0]
+    assert np.allclose(a[hit], np.float32([0.8, 0.4, 0.2])) and np.allclose(a[~hit], np.float32([0.25, 0.5, 0.75]))
+    assert np.allclose(np.linalg.norm(n[hit], axis=1), 1.0, atol=1e-5)
+    assert n[H // 2, W // 2, 2] > 0.99  # facing the camera
+    av = oracle.tonemap(W, H, a.reshape(-1), np.zeros(W * H, np.uint32), 0, massrt.DISPLAY_ALBEDO)
+    nv = oracle.tonemap(W, H, n.reshape(-1), np.zeros(W * H, np.uint32), 0, massrt.DISPLAY_NORMAL)
+    assert tuple(av[0, 0]) == tuple(np.floor(np.float32([0.25, 0.5, 0.75]) ** np.float32(1 / 2.2) * 255).astype(int))
+    assert tuple(nv[0, 0]) == (127, 127, 127)  # (0 + 1) / 2 * 255 = 127.5 -> 127
+    # deterministic for a fixed seed
+    a2, _ = o.prepass(W, H, seed=5)
+    assert np.array_equal(a2, a.reshape(-1))
