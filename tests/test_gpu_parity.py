@@ -4,6 +4,8 @@ Bar (BASELINE.json north_star): closest-hit ids / t / front_face, bounce
 counts and traversal counters bit-exact; radiance within 1e-4 relative L2
 (RTOL below). The GPU folds radiance forward (T *= atten) where the reference
 recursion folds it post-order (world.rs:71-72), so radiance differs by ULPs."""
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -366,3 +368,24 @@ def test_prepass_matches_oracle(ctx, small_scenes, scene):
     zeros = np.zeros(W * H, np.uint32)
     for mode, buf in ((massrt.DISPLAY_ALBEDO, ga), (massrt.DISPLAY_NORMAL, gn)):
         assert np.array_equal(ctx.tonemap(W, H, buf, zeros, 1, mode), oracle.tonemap(W, H, buf, zeros, 1, mode))
+
+
+def test_cpp_driver_writes_the_same_image(ctx, small_scenes, golden_dir, tmp_path):
+    """examples/mrt_render.cpp (the render()+dump() driver over the C ABI)
+    produces exactly the bytes the library's render + tonemap give."""
+    import subprocess
+    from PIL import Image
+    exe = Path(massrt.__file__).parent / "mrt_render"
+    out = tmp_path / "cornell.png"
+    r = subprocess.run([str(exe), "cornell", "64", "36", "4", str(out), str(golden_dir)], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    b, _ = small_scenes["cornell"]
+    ctx.upload(b)
+    rgb, bo = ctx.render(64, 36, 0, 4, seed=1)
+    for suffix, mode in (("", massrt.DISPLAY_DEFAULT), ("_depth", massrt.DISPLAY_DEPTH)):
+        png = np.asarray(Image.open(tmp_path / f"cornell{suffix}.png").convert("RGB"))
+        assert np.array_equal(png, ctx.tonemap(64, 36, rgb, bo, 4, mode)), suffix
+    a, n = ctx.prepass(64, 36, seed=1)
+    png = np.asarray(Image.open(tmp_path / "cornell_normal.png").convert("RGB"))
+    assert np.array_equal(png, ctx.tonemap(64, 36, n, bo, 4, massrt.DISPLAY_NORMAL))
