@@ -26,6 +26,8 @@
 namespace mrt {
 
 enum : uint32_t { KIND_BOX = 1, KIND_SPHERE = 2, KIND_TRI = 3, KIND_INST = 4, KIND_MODEL = 5 };
+// traversal-only pseudo-kind: the region being traversed has ended (path.h)
+constexpr uint32_t KIND_END = 0;
 enum : uint32_t { TRI_FLAG_ALPHA = 1u, TRI_FLAG_UV = 2u };
 
 // Flattened material: surface resolved in place.

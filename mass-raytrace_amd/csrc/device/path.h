@@ -393,24 +393,14 @@ MRT_DEV TRay world_ray(const TravIn& in, uint32_t ray) {
   return make_tray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, in.S.fast_ok);
 }
 
-// Move to record t.i (leaving a finished BLAS region) and prefetch it.
+// Load record t.i, or mark the end of the region being traversed with the
+// pseudo-kind KIND_END (handled by trav_prim: leave the BLAS, or finish).
+// Keeping the rare BLAS exit out of this step keeps the box step small.
 MRT_DEV void trav_fetch(const TravIn& in, Trav& t) {
   const DevScene& S = in.S;
   if (t.i >= t.end) {
-    if (t.ret == kNoRet) {
-      t.done = true;
-      return;
-    }
-    // leave the BLAS: back to the world ray (geom.rs:405-409); a model
-    // shares the world ray, an instance's object-space ray is replaced
-    if (t.ret & kRetInstance) t.r = world_ray(in, t.ray);
-    t.i = t.ret & ~kRetInstance;
-    t.end = S.world_end;
-    t.ret = kNoRet;
-    if (t.i >= t.end) {
-      t.done = true;
-      return;
-    }
+    t.s1.w = KIND_END;
+    return;
   }
 #ifdef MRT_DEBUG_BOUNDS
   if (t.i + 1 >= S.n_slots || ++t.steps > (1u << 24)) {  // record and stop instead of looping/faulting
@@ -421,6 +411,21 @@ MRT_DEV void trav_fetch(const TravIn& in, Trav& t) {
 #endif
   t.s0 = in.slots[MRT_IDX(S, t.i, S.n_slots, 5)];
   t.s1 = in.slots[MRT_IDX(S, t.i + 1, S.n_slots, 6)];
+}
+
+// The region ended: leave the BLAS back to the world ray (geom.rs:405-409;
+// a model shares the world ray, an instance's object-space ray is replaced),
+// or finish the ray.
+MRT_DEV void trav_end(const TravIn& in, Trav& t) {
+  if (t.ret == kNoRet) {
+    t.done = true;
+    return;
+  }
+  if (t.ret & kRetInstance) t.r = world_ray(in, t.ray);
+  t.i = t.ret & ~kRetInstance;
+  t.end = in.S.world_end;
+  t.ret = kNoRet;
+  trav_fetch(in, t);
 }
 
 // Start ray `ray` of the pool (World::intersect(ray, in.tmin, tmax)).
@@ -459,6 +464,10 @@ MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
   const DevScene& S = in.S;
   const uint4 s0 = t.s0, s1 = t.s1;
   const uint32_t kind = s1.w;
+  if (kind == KIND_END) {
+    trav_end(in, t);
+    return;
+  }
   if (kind == KIND_TRI) {
     if (COUNT) lc.triangle_tests++;
     const uint4 s2 = in.slots[MRT_IDX(S, t.i + 2, S.n_slots, 7)];

@@ -160,7 +160,8 @@ constexpr uint64_t kResultsMax = 256ull << 20;  // samples per results slab (4 G
 struct TraceTune {
   uint32_t chunk = 128;     // rays per atomic grab
   uint32_t refill = 32;      // refill once this many lanes idle
-  uint32_t prim_batch = 16;  // run the primitive branch once this many lanes wait at one
+  uint32_t prim_batch = 1;   // run the primitive branch once this many lanes wait at one
+  uint32_t box_min = 24;     // inner box loop while this many lanes are at a box (65: off)
   uint32_t shade_batch = 16; // k_render: shade once this many lanes finished a segment
 };
 
@@ -231,6 +232,17 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
     }
 #pragma unroll
     for (int q = 0; q < R; ++q) {
+      // box run: keep stepping boxes with little per-step overhead while at
+      // least tune.box_min lanes are at one (lanes reaching a primitive wait)
+      for (;;) {
+        const bool at_box = !t[q].done && trav_at_box(t[q]);
+        if ((uint32_t)__popcll(__ballot(at_box)) < tune.box_min) break;
+        if (at_box) trav_box<COUNT>(tin, t[q], lc);
+        if (COUNT) {
+          lc.wave_slots += lane_id() == 0 ? 64u : 0u;
+          lc.lane_steps += at_box ? 1u : 0u;
+        }
+      }
       const bool busy = !t[q].done;  // idle lanes hold a done Trav
       const bool at_box = busy && trav_at_box(t[q]);
       const unsigned long long box_mask = __ballot(at_box);
@@ -1255,6 +1267,7 @@ int mrt_create(int device, mrt_ctx** out) {
     if (const char* e = getenv("MRT_TRACE_REFILL")) c->tune.refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_PRIM_BATCH")) c->tune.prim_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_CHUNK")) c->tune.chunk = (uint32_t)std::max(64, atoi(e));
+    if (const char* e = getenv("MRT_TRACE_BOX_MIN")) c->tune.box_min = (uint32_t)std::max(1, std::min(65, atoi(e)));
     if (const char* e = getenv("MRT_SHADE_BATCH")) c->tune.shade_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_POOL_PATHS")) c->pool_paths = (size_t)std::max(1 << 16, std::min(1 << 28, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_RAYS_PER_LANE")) c->rays_per_lane = atoi(e) == 2 ? 2 : 1;
