@@ -312,7 +312,7 @@ MRT_DEV bool shade_step(const DevScene& S, uint32_t max_depth, const Hit& h, V3&
 }
 
 template <bool COUNT>
-__global__ __launch_bounds__(kBlock) void k_shade(DevScene S, DevCamera cam, RenderParams rp, PathBufs in,
+__global__ __launch_bounds__(kBlock, 8) void k_shade(DevScene S, DevCamera cam, RenderParams rp, PathBufs in,
                                                   PathBufs out, const uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   uint32_t* work, float4* results, DevCounters* cnt) {
   const uint32_t n = ctrl->active[cur];
