@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 1
+#define MRT_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 #define MRT_OK 0
@@ -104,11 +104,15 @@ typedef struct {
 #define MRT_MAT_METAL 2u         /* material.rs:248-284 (param = fuzz, clamped) */
 #define MRT_MAT_DIELECTRIC 3u    /* material.rs:286-329 (param = refraction index) */
 #define MRT_MAT_DIFFUSE_LIGHT 4u /* material.rs:227-246 (emit) */
+#define MRT_MAT_SPECULAR 5u      /* material.rs:331-378 (param = refraction index; surface of the inner Lambertian) */
+#define MRT_MAT_ISOTROPHIC 6u    /* material.rs:428-445 (emit[] holds the albedo) */
+#define MRT_MAT_MIX 7u           /* material.rs:391-426 (param = ratio; left, right = material indices < own) */
 typedef struct {
   uint32_t kind;
-  uint32_t surface; /* index into surfaces (Lambertian/Metal) */
+  uint32_t surface; /* index into surfaces (Lambertian/Metal/Specular) */
   float param;
   float emit[3];
+  uint32_t left, right; /* Mix only */
 } mrt_material;
 
 #define MRT_SURF_SOLID 0u   /* SolidColor  texture.rs:179-194 */
@@ -285,6 +289,8 @@ int mrt_builder_solid(mrt_builder* b, float r, float g, float bl, float a);
 int mrt_builder_texture_png(mrt_builder* b, const char* path, uint32_t wrap);
 int mrt_builder_texture_rgba(mrt_builder* b, const uint8_t* rgba, uint32_t w, uint32_t h, uint32_t wrap);
 int mrt_builder_material(mrt_builder* b, uint32_t kind, uint32_t surface, float param, float er, float eg, float eb);
+/* Mix::new(ratio, left, right): returns the material index */
+int mrt_builder_mix(mrt_builder* b, float ratio, uint32_t left, uint32_t right);
 int mrt_builder_background(mrt_builder* b, uint32_t kind, uint32_t surface, float r, float g, float bl);
 /* world objects (World::add, world.rs:112-115) */
 int mrt_builder_add_sphere(mrt_builder* b, uint32_t material, float cx, float cy, float cz, float radius);

@@ -35,8 +35,9 @@ enum : uint32_t { TRI_FLAG_ALPHA = 1u, TRI_FLAG_UV = 2u };
 //   q1 = {color/emit rgba as float bits}
 struct GpuMaterial {
   uint32_t kind, surf_kind, texture;
-  float param;
-  float color[4];  // SolidColor rgba (Lambertian/Metal) or emit rgb (DiffuseLight)
+  float param;     // Metal fuzz, Dielectric/Specular refraction index, Mix ratio
+  float color[4];  // SolidColor rgba (Lambertian/Metal/Specular), emit rgb (DiffuseLight), albedo (Isotrophic)
+  uint32_t left, right, pad0, pad1;  // Mix children
 };
 
 struct GpuTexture {

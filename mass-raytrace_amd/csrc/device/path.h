@@ -256,7 +256,8 @@ MRT_DEV bool tri_alpha_pass(const DevScene& S, uint32_t id, V3 o, V3 d, float t,
   tri_bary(s, point, a0, a1, a2);
   V2 uv = (s.uva * a0 + s.uvb * a1) + s.uvc * a2;
   const GpuMaterial m = S.materials[MRT_IDX(S, s.material, S.n_materials, 4)];
-  if (m.kind != MRT_MAT_LAMBERTIAN && m.kind != MRT_MAT_METAL) return true;
+  // Lambertian/Metal alpha_test; Specular's forwards to its inner Lambertian
+  if (m.kind != MRT_MAT_LAMBERTIAN && m.kind != MRT_MAT_METAL && m.kind != MRT_MAT_SPECULAR) return true;
   return surface_get_f(S, m, uv, lc).w != 0.0f;
 }
 
@@ -647,20 +648,40 @@ MRT_DEV V3 background(const DevScene& S, V3 d, LocalCounters& lc) {
 
 // Hit::emit + Hit::scatter (geom.rs:26-32). Returns true when the path
 // continues with (new_o, new_d) and attenuation `atten`.
+// Mix::scatter/emit/alpha_test (material.rs:402-424): every call draws once
+// to pick a side, recursively; children precede their Mix in the table.
+MRT_DEV uint32_t mix_pick(const DevScene& S, uint32_t mi, PathRng& rng) {
+  for (;;) {
+    const GpuMaterial m = S.materials[MRT_IDX(S, mi, S.n_materials, 4)];
+    if (m.kind != MRT_MAT_MIX) return mi;
+    mi = rng.f32() < m.param ? m.left : m.right;
+  }
+}
+
+// Lambertian::scatter (material.rs:203-215)
+MRT_DEV void lambertian(const DevScene& S, const GpuMaterial& m, const Surf& s, PathRng& rng, V3& atten, V3& new_d,
+                        LocalCounters& lc) {
+  V3 dir = s.normal + unit(random_in_unit_sphere(rng));
+  if (near_zero(dir)) dir = s.normal;
+  V4 c = surface_get_f(S, m, s.has_uv ? s.uv : V2{0, 0}, lc);
+  atten = V3{c.x, c.y, c.z};
+  new_d = dir;
+}
+
+// Hit::emit then Hit::scatter (world.rs:69-70), in that order of RNG draws.
 MRT_DEV bool scatter(const DevScene& S, const Surf& s, V3 d, PathRng& rng, V3& emitted, V3& atten, V3& new_d,
                      LocalCounters& lc) {
-  const GpuMaterial m = S.materials[MRT_IDX(S, s.material, S.n_materials, 4)];
   emitted = V3{0, 0, 0};
+  {
+    const GpuMaterial e = S.materials[mix_pick(S, s.material, rng)];
+    if (e.kind == MRT_MAT_DIFFUSE_LIGHT) emitted = V3{e.color[0], e.color[1], e.color[2]};
+  }
+  const GpuMaterial m = S.materials[mix_pick(S, s.material, rng)];
   V2 uv = s.has_uv ? s.uv : V2{0, 0};
   switch (m.kind) {
-    case MRT_MAT_LAMBERTIAN: {
-      V3 dir = s.normal + unit(random_in_unit_sphere(rng));
-      if (near_zero(dir)) dir = s.normal;
-      V4 c = surface_get_f(S, m, uv, lc);
-      atten = V3{c.x, c.y, c.z};
-      new_d = dir;
+    case MRT_MAT_LAMBERTIAN:
+      lambertian(S, m, s, rng, atten, new_d, lc);
       return true;
-    }
     case MRT_MAT_METAL: {
       V3 reflected = reflect(unit(d), s.normal);
       V3 dir = reflected + (random_in_unit_sphere(rng) * m.param);
@@ -672,23 +693,29 @@ MRT_DEV bool scatter(const DevScene& S, const Surf& s, V3 d, PathRng& rng, V3& e
       }
       return false;
     }
-    case MRT_MAT_DIELECTRIC: {
+    case MRT_MAT_DIELECTRIC:
+    case MRT_MAT_SPECULAR: {  // material.rs:299-328 / 355-377
       float ratio = s.front_face ? 1.0f / m.param : m.param;
       V3 ud = unit(d);
       float cos_theta = fminf(dot(-ud, s.normal), 1.0f);
       float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
       bool cannot_refract = ratio * sin_theta > 1.0f;
-      if (cannot_refract || reflectance(cos_theta, ratio) > rng.f32())
+      if (cannot_refract || reflectance(cos_theta, ratio) > rng.f32()) {
         new_d = reflect(ud, s.normal);
-      else
+      } else if (m.kind == MRT_MAT_SPECULAR) {
+        lambertian(S, m, s, rng, atten, new_d, lc);  // return self.inner.scatter(ray, hit)
+        return true;
+      } else {
         new_d = refract(ud, s.normal, ratio);
+      }
       atten = fill3(1.0f);
       return true;
     }
-    case MRT_MAT_DIFFUSE_LIGHT:
-      emitted = V3{m.color[0], m.color[1], m.color[2]};
-      return false;
-    default:
+    case MRT_MAT_ISOTROPHIC:  // material.rs:438-444: direction not normalised
+      atten = V3{m.color[0], m.color[1], m.color[2]};
+      new_d = random_in_unit_sphere(rng);
+      return true;
+    default:  // DiffuseLight, ()
       return false;
   }
 }

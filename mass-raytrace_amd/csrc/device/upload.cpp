@@ -84,10 +84,15 @@ struct Emitter {
   // Triangle::intersect runs alpha_test only with uvs; it can reject only if
   // the triangle's own material samples a texture holding a zero alpha.
   std::vector<int8_t> tex_zero_alpha;  // per texture, computed once
+  bool mix_alpha = false;              // a uv triangle's alpha test draws random numbers
   bool needs_alpha(const mrt_triangle& t) {
     if (!(t.flags & MRT_TRI_HAS_UV) || t.material >= d.n_materials) return false;
     const mrt_material& m = d.materials[t.material];
-    if (m.kind != MRT_MAT_LAMBERTIAN && m.kind != MRT_MAT_METAL) return false;
+    if (m.kind == MRT_MAT_MIX) {  // Mix::alpha_test draws from the path RNG (material.rs:418-424)
+      mix_alpha = true;
+      return true;
+    }
+    if (m.kind != MRT_MAT_LAMBERTIAN && m.kind != MRT_MAT_METAL && m.kind != MRT_MAT_SPECULAR) return false;
     if (m.surface >= d.n_surfaces) return false;
     const mrt_surface& sf = d.surfaces[m.surface];
     if (sf.kind == MRT_SURF_SOLID) return sf.color[3] == 0.0f;
@@ -172,16 +177,21 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
     GpuMaterial g{};
     g.kind = m.kind;
     g.param = m.param;
-    if (m.kind > MRT_MAT_DIFFUSE_LIGHT) return (err = "bad material kind", false);
-    if (m.kind == MRT_MAT_LAMBERTIAN || m.kind == MRT_MAT_METAL) {
+    if (m.kind > MRT_MAT_MIX) return (err = "bad material kind", false);
+    if (m.kind == MRT_MAT_LAMBERTIAN || m.kind == MRT_MAT_METAL || m.kind == MRT_MAT_SPECULAR) {
       if (m.surface >= d.n_surfaces) return (err = "material surface out of range", false);
       const mrt_surface& sf = d.surfaces[m.surface];
       g.surf_kind = sf.kind;
       g.texture = sf.texture;
       if (sf.kind == MRT_SURF_TEXTURE && sf.texture >= d.n_textures) return (err = "surface texture out of range", false);
       for (int k = 0; k < 4; ++k) g.color[k] = sf.color[k];
-    } else if (m.kind == MRT_MAT_DIFFUSE_LIGHT) {
-      for (int k = 0; k < 3; ++k) g.color[k] = m.emit[k];
+    } else if (m.kind == MRT_MAT_DIFFUSE_LIGHT || m.kind == MRT_MAT_ISOTROPHIC) {
+      for (int k = 0; k < 3; ++k) g.color[k] = m.emit[k];  // emission / albedo
+    } else if (m.kind == MRT_MAT_MIX) {
+      // children strictly below: the device's pick loop always terminates
+      if (m.left >= i || m.right >= i) return (err = "Mix children must precede the Mix in the material table", false);
+      g.left = m.left;
+      g.right = m.right;
     }
     s.materials.push_back(g);
   }
@@ -265,6 +275,9 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
     s.slots[4 * p.first + 1] = it->second.first;
     s.slots[4 * p.first + 2] = it->second.second;
   }
+  if (e.mix_alpha)
+    return (err = "a Mix material on a triangle with uvs (its alpha test draws random numbers during traversal) "
+                  "is not supported yet", false);
   if (s.slots.size() / 4 >= 0x80000000ull) return (err = "scene too large (record stream >= 2^31 slots)", false);
   return true;
 }

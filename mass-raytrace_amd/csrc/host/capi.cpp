@@ -102,7 +102,7 @@ int mrt_builder_texture_rgba(mrt_builder* b, const uint8_t* rgba, uint32_t w, ui
 int mrt_builder_material(mrt_builder* b, uint32_t kind, uint32_t surface, float param, float er, float eg, float eb) {
   return guard(b, [&] {
     Surface s;
-    if (kind == MRT_MAT_LAMBERTIAN || kind == MRT_MAT_METAL) {
+    if (kind == MRT_MAT_LAMBERTIAN || kind == MRT_MAT_METAL || kind == MRT_MAT_SPECULAR) {
       if (surface >= b->surfaces.size()) throw Error(MRT_ERR_INVALID, "surface index out of range");
       s = b->surfaces[surface];
     }
@@ -123,10 +123,25 @@ int mrt_builder_material(mrt_builder* b, uint32_t kind, uint32_t surface, float 
       case MRT_MAT_DIFFUSE_LIGHT:
         m = DiffuseLight(V3{er, eg, eb});
         break;
+      case MRT_MAT_SPECULAR:
+        m = Specular(param, s);
+        break;
+      case MRT_MAT_ISOTROPHIC:
+        m = Isotrophic(V3{er, eg, eb});
+        break;
       default:
         throw Error(MRT_ERR_INVALID, "bad material kind");
     }
     b->materials.push_back(m);
+    return (int)b->materials.size() - 1;
+  });
+}
+
+int mrt_builder_mix(mrt_builder* b, float ratio, uint32_t left, uint32_t right) {
+  return guard(b, [&] {
+    if (left >= b->materials.size() || right >= b->materials.size())
+      throw Error(MRT_ERR_INVALID, "material index out of range");
+    b->materials.push_back(Mix(ratio, b->materials[left], b->materials[right]));
     return (int)b->materials.size() - 1;
   });
 }

@@ -166,9 +166,15 @@ uint32_t World::intern_surface(const Surface& s) {
 uint32_t World::intern_material(const Material& m) {
   mrt_material d{};
   d.kind = m.kind;
-  d.surface = (m.kind == MRT_MAT_LAMBERTIAN || m.kind == MRT_MAT_METAL) ? intern_surface(m.surface) : 0;
+  d.surface = (m.kind == MRT_MAT_LAMBERTIAN || m.kind == MRT_MAT_METAL || m.kind == MRT_MAT_SPECULAR)
+                  ? intern_surface(m.surface)
+                  : 0;
   d.param = m.param;
   put3(d.emit, m.emit);
+  if (m.kind == MRT_MAT_MIX) {  // children first: their indices are lower than this one's
+    d.left = intern_material(*m.left);
+    d.right = intern_material(*m.right);
+  }
   std::string key((const char*)&d, sizeof(d));
   auto it = material_index_.find(key);
   if (it != material_index_.end()) return it->second;

@@ -84,7 +84,8 @@ struct Material {
   uint32_t kind = MRT_MAT_NONE;
   Surface surface;
   float param = 0.0f;
-  V3 emit{0, 0, 0};
+  V3 emit{0, 0, 0};                             // DiffuseLight emission / Isotrophic albedo
+  std::shared_ptr<const Material> left, right;  // Mix
 };
 inline Material NoMaterial() { return Material{}; }  // impl Material for ()
 inline Material Lambertian(Surface s) {
@@ -104,6 +105,27 @@ inline Material Dielectric(float refraction_index) {
   Material m;
   m.kind = MRT_MAT_DIELECTRIC;
   m.param = refraction_index;
+  return m;
+}
+inline Material Specular(float refraction_index, Surface s) {  // material.rs:338-345
+  Material m;
+  m.kind = MRT_MAT_SPECULAR;
+  m.param = refraction_index;
+  m.surface = std::move(s);
+  return m;
+}
+inline Material Isotrophic(V3 albedo) {  // material.rs:432-436
+  Material m;
+  m.kind = MRT_MAT_ISOTROPHIC;
+  m.emit = albedo;
+  return m;
+}
+inline Material Mix(float ratio, Material l, Material r) {  // material.rs:396-400
+  Material m;
+  m.kind = MRT_MAT_MIX;
+  m.param = ratio;
+  m.left = std::make_shared<const Material>(std::move(l));
+  m.right = std::make_shared<const Material>(std::move(r));
   return m;
 }
 inline Material DiffuseLight(V3 emit) {

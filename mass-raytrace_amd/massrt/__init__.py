@@ -26,8 +26,9 @@ LIB_PATH = (Path(_SEL) if _SEL.endswith(".so") else
 REPO = _HERE.parent.parent
 
 # ---- constants (massrt.h) --------------------------------------------------
+ABI_VERSION = 2  # MRT_ABI_VERSION this binding was written for
 REF_NONE, REF_NODE, REF_SPHERE, REF_TRIANGLE, REF_INSTANCE, REF_MODEL = range(6)
-MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT = range(5)
+MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_SPECULAR, MAT_ISOTROPHIC, MAT_MIX = range(8)
 WRAP_MIRROR, WRAP_REPEAT, WRAP_CLAMP = range(3)
 BG_SOLID, BG_SKY, BG_SKYSPHERE = range(3)
 NO_MATERIAL = 0xFFFFFFFF
@@ -74,7 +75,8 @@ class MrtModel(C.Structure):
 
 
 class MrtMaterial(C.Structure):
-    _fields_ = [("kind", C.c_uint32), ("surface", C.c_uint32), ("param", C.c_float), ("emit", C.c_float * 3)]
+    _fields_ = [("kind", C.c_uint32), ("surface", C.c_uint32), ("param", C.c_float), ("emit", C.c_float * 3),
+                ("left", C.c_uint32), ("right", C.c_uint32)]
 
 
 class MrtSurface(C.Structure):
@@ -157,7 +159,8 @@ EXPORTED_SYMBOLS = [
     "mrt_get_counters", "mrt_reset_counters", "mrt_scene_device_bytes", "mrt_get_kernel_stats",
     "mrt_reset_kernel_stats", "mrt_selftest_division", "mrt_selftest_slab", "mrt_debug_status", "mrt_debug_build",
     "mrt_builder_new", "mrt_builder_free", "mrt_builder_builtin", "mrt_builder_rand_f32", "mrt_builder_solid",
-    "mrt_builder_texture_png", "mrt_builder_texture_rgba", "mrt_builder_material", "mrt_builder_background",
+    "mrt_builder_texture_png", "mrt_builder_texture_rgba", "mrt_builder_material", "mrt_builder_mix",
+    "mrt_builder_background",
     "mrt_builder_add_sphere", "mrt_builder_add_triangle", "mrt_builder_model", "mrt_builder_model_from_ply",
     "mrt_builder_add_instance", "mrt_builder_camera", "mrt_builder_build_bvh", "mrt_builder_desc",
     "mrt_builder_last_error", "mrt_load_ply", "mrt_load_stl", "mrt_load_obj",
@@ -208,6 +211,7 @@ def lib() -> C.CDLL:
         "mrt_builder_texture_rgba": (I, [P, C.POINTER(C.c_uint8), U32, U32, U32]),
         "mrt_builder_material": (I, [P, U32, U32, F, F, F, F]),
         "mrt_builder_background": (I, [P, U32, U32, F, F, F]),
+        "mrt_builder_mix": (I, [P, F, U32, U32]),
         "mrt_builder_add_sphere": (I, [P, U32, F, F, F, F]),
         "mrt_builder_add_triangle": (I, [P, U32, fp]),
         "mrt_builder_model": (I, [P, U32, U32, fp, U32, I, I]),
@@ -295,6 +299,10 @@ class Builder:
 
     def material(self, kind, surface=0, param=0.0, emit=(0.0, 0.0, 0.0)) -> int:
         return _check_builder(lib().mrt_builder_material(self.h, kind, surface, param, *emit))
+
+    def mix(self, ratio, left, right) -> int:
+        """Mix::new(ratio, left, right) (material.rs:391-426)."""
+        return _check_builder(lib().mrt_builder_mix(self.h, ratio, left, right))
 
     def background(self, kind, surface=0, color=(0.0, 0.0, 0.0)):
         _check_builder(lib().mrt_builder_background(self.h, kind, surface, *color))

@@ -45,6 +45,7 @@ def lib() -> C.CDLL:
         "orc_texture_png": (I, [P, C.c_char_p, U32]),
         "orc_material": (I, [P, U32, U32, F, F, F, F]),
         "orc_background": (I, [P, U32, U32, F, F, F]),
+        "orc_mix": (I, [P, F, U32, U32]),
         "orc_add_sphere": (I, [P, U32, F, F, F, F]),
         "orc_add_triangle": (I, [P, U32, fp]),
         "orc_model": (I, [P, U32, U32, fp, U32, I, I]),
@@ -167,6 +168,9 @@ class Scene:
 
     def material(self, kind, surface=0, param=0.0, emit=(0.0, 0.0, 0.0)):
         return self._chk(lib().orc_material(self.h, kind, surface, param, *emit))
+
+    def mix(self, ratio, left, right):
+        return self._chk(lib().orc_mix(self.h, ratio, left, right))
 
     def background(self, kind, surface=0, color=(0.0, 0.0, 0.0)):
         self._chk(lib().orc_background(self.h, kind, surface, *color))

@@ -299,7 +299,7 @@ struct Scatter {
 struct Material {  // material.rs:15-27
   virtual ~Material() {}
   virtual bool scatter(const Ray& ray, const Hit& hit, Ctx& c, Scatter& out) const = 0;
-  virtual bool emit(const Hit&, V3&) const { return false; }
+  virtual bool emit(const Hit&, Ctx&, V3&) const { return false; }
   virtual bool alpha_test(V2, Ctx&) const { return true; }
 };
 struct NoMaterial : Material {  // material.rs:385-389
@@ -370,11 +370,53 @@ struct Dielectric : Material {  // material.rs:286-329
     return true;
   }
 };
+struct Specular : Material {  // material.rs:331-378: Dielectric-style reflect, else the inner Lambertian
+  float ior;
+  Lambertian inner;
+  Specular(float i, std::shared_ptr<Surface> s) : ior(i), inner(std::move(s)) {}
+  bool scatter(const Ray& ray, const Hit& hit, Ctx& c, Scatter& out) const override {
+    float ratio = hit.front_face ? 1.0f / ior : ior;
+    V3 ud = unit(ray.direction);
+    float cos_theta = fminf(dot(-ud, hit.normal), 1.0f);
+    float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
+    bool cannot = ratio * sin_theta > 1.0f;
+    if (cannot || Dielectric::reflectance(cos_theta, ratio) > c.rand()) {
+      out.attenuation = fill(1.0f);
+      out.scattered = Ray{hit.point, reflect(ud, hit.normal)};
+      return true;
+    }
+    return inner.scatter(ray, hit, c, out);
+  }
+  bool alpha_test(V2 uv, Ctx& c) const override { return inner.alpha_test(uv, c); }
+};
+struct Mix : Material {  // material.rs:391-426: every call draws to pick a side
+  float ratio;
+  std::shared_ptr<Material> left, right;
+  Mix(float r, std::shared_ptr<Material> l, std::shared_ptr<Material> rr) : ratio(r), left(std::move(l)), right(std::move(rr)) {}
+  bool scatter(const Ray& ray, const Hit& hit, Ctx& c, Scatter& out) const override {
+    return c.rand() < ratio ? left->scatter(ray, hit, c, out) : right->scatter(ray, hit, c, out);
+  }
+  bool emit(const Hit& hit, Ctx& c, V3& out) const override {
+    return c.rand() < ratio ? left->emit(hit, c, out) : right->emit(hit, c, out);
+  }
+  bool alpha_test(V2 uv, Ctx& c) const override {
+    return c.rand() < ratio ? left->alpha_test(uv, c) : right->alpha_test(uv, c);
+  }
+};
+struct Isotrophic : Material {  // material.rs:428-445
+  V3 albedo;
+  explicit Isotrophic(V3 a) : albedo(a) {}
+  bool scatter(const Ray&, const Hit& hit, Ctx& c, Scatter& out) const override {
+    out.attenuation = albedo;
+    out.scattered = Ray{hit.point, random_in_unit_sphere(c)};
+    return true;
+  }
+};
 struct DiffuseLight : Material {  // material.rs:227-246
   V3 e;
   explicit DiffuseLight(V3 v) : e(v) {}
   bool scatter(const Ray&, const Hit&, Ctx&, Scatter&) const override { return false; }
-  bool emit(const Hit&, V3& out) const override {
+  bool emit(const Hit&, Ctx&, V3& out) const override {
     out = e;
     return true;
   }
@@ -711,7 +753,7 @@ static std::pair<V3, uint32_t> trace(const World& w, const Ray& ray, uint32_t de
   Hit hit;
   if (w.intersect(ray, 0.001f, INFINITY, hit, c)) {
     V3 emitted{0, 0, 0};
-    hit.material->emit(hit, emitted);
+    hit.material->emit(hit, c, emitted);
     Scatter s;
     if (hit.material->scatter(ray, hit, c, s)) {
       c.cnt.bounces++;
@@ -1270,10 +1312,23 @@ int orc_material(orc_scene* s, uint32_t kind, uint32_t surface, float param, flo
       case 4:
         m = std::make_shared<DiffuseLight>(V3{er, eg, eb});
         break;
+      case 5:
+        m = std::make_shared<Specular>(param, surf());
+        break;
+      case 6:
+        m = std::make_shared<Isotrophic>(V3{er, eg, eb});
+        break;
       default:
         throw std::runtime_error("bad material kind");
     }
     s->materials.push_back(m);
+    return (int)s->materials.size() - 1;
+  });
+}
+int orc_mix(orc_scene* s, float ratio, uint32_t left, uint32_t right) {
+  return guard([&] {
+    if (left >= s->materials.size() || right >= s->materials.size()) throw std::runtime_error("material out of range");
+    s->materials.push_back(std::make_shared<Mix>(ratio, s->materials[left], s->materials[right]));
     return (int)s->materials.size() - 1;
   });
 }
@@ -1602,7 +1657,7 @@ int orc_prepass(orc_scene* s, uint32_t W, uint32_t H, uint64_t seed, int threads
           Hit hit;
           if (s->world.intersect(ray, 0.001f, INFINITY, hit, c)) {
             V3 emitted{0, 0, 0};
-            hit.material->emit(hit, emitted);
+            hit.material->emit(hit, c, emitted);
             Scatter sc;
             a = hit.material->scatter(ray, hit, c, sc) ? sc.attenuation : emitted;
             n = hit.normal;

@@ -45,6 +45,10 @@ int orc_solid(orc_scene* s, float r, float g, float b, float a);
 int orc_texture_rgba(orc_scene* s, const uint8_t* rgba, uint32_t w, uint32_t h, uint32_t wrap);
 int orc_texture_png(orc_scene* s, const char* path, uint32_t wrap);
 int orc_material(orc_scene* s, uint32_t kind, uint32_t surface, float param, float er, float eg, float eb);
+// Mix::new(ratio, left, right) (material.rs:391-426); kinds 5 Specular
+// (param = refraction index, surface) and 6 Isotrophic (albedo = er,eg,eb) go
+// through orc_material.
+int orc_mix(orc_scene* s, float ratio, uint32_t left, uint32_t right);
 int orc_background(orc_scene* s, uint32_t kind, uint32_t surface, float r, float g, float b);
 int orc_add_sphere(orc_scene* s, uint32_t material, float cx, float cy, float cz, float radius);
 int orc_add_triangle(orc_scene* s, uint32_t material, const float* abc);

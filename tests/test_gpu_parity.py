@@ -389,3 +389,36 @@ def test_cpp_driver_writes_the_same_image(ctx, small_scenes, golden_dir, tmp_pat
     a, n = ctx.prepass(64, 36, seed=1)
     png = np.asarray(Image.open(tmp_path / "cornell_normal.png").convert("RGB"))
     assert np.array_equal(png, ctx.tonemap(64, 36, n, bo, 4, massrt.DISPLAY_NORMAL))
+
+
+def test_extended_materials_parity(ctx):
+    """Specular, Isotrophic and (nested) Mix, including a Mix whose emit draws
+    (material.rs:331-445): GPU render/pre-pass vs the oracle."""
+    def scene(x):
+        x.background(massrt.BG_SKY)
+        red, grey = x.solid(0.9, 0.2, 0.2, 1.0), x.solid(0.6, 0.6, 0.6, 1.0)
+        spec = x.material(massrt.MAT_SPECULAR, red, 1.8)
+        iso = x.material(massrt.MAT_ISOTROPHIC, 0, 0.0, (0.4, 0.7, 0.3))
+        lamb = x.material(massrt.MAT_LAMBERTIAN, grey)
+        light = x.material(massrt.MAT_DIFFUSE_LIGHT, 0, 0.0, (4.0, 4.0, 3.0))
+        mix = x.mix(0.35, lamb, spec)
+        glow = x.mix(0.5, light, x.mix(0.25, x.material(massrt.MAT_METAL, grey, 0.3), x.material(massrt.MAT_DIELECTRIC, 0, 1.5)))
+        x.add_sphere(lamb, (0, -100.5, -1), 100.0)
+        for k, m in enumerate([spec, iso, mix, glow, spec, mix]):
+            x.add_sphere(m, (-2.5 + k, 0.0, -1.0 - 0.3 * (k % 2)), 0.45)
+        x.build_bvh()
+        x.camera(50.0, (0, 1, 3), (0, 0, -1), aspect=ASPECT)
+    b, o = build_both(scene)
+    ctx.upload(b)
+    ctx.reset_counters()
+    o.reset_counters()
+    rgb, bo = ctx.render(64, 36, 0, 4, seed=21, counters=True)
+    orgb, obo = o.render(64, 36, 0, 4, seed=21)
+    assert np.array_equal(bo, obo)
+    assert rel_l2(rgb, orgb) <= RTOL
+    gc, oc = ctx.counters(), o.counters()
+    for k in ["samples", "segments", "node_visits", "sphere_tests", "closest_hits", "bounces"]:
+        assert gc[k] == oc[k], (k, gc[k], oc[k])
+    ga, gn = ctx.prepass(64, 36, seed=2)
+    oa, on = o.prepass(64, 36, seed=2)
+    assert np.array_equal(gn, on) and np.array_equal(ga, oa)

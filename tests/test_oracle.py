@@ -134,3 +134,30 @@ def test_depth_limits(golden_dir):
     assert not rgb.any() and not b.any()  # trace(ray, 0) = (0, 0) (world.rs:66-67)
     rgb, b = o.render(16, 9, 0, 2, seed=1, max_depth=1, threads=2)
     assert b.max() <= 2
+
+
+@pytest.mark.parametrize("variant", ["specular", "isotrophic", "mix", "mix_nested"])
+def test_extended_materials_furnace(variant):
+    """Specular (material.rs:331-378), Isotrophic (428-445) and Mix (391-426)
+    with white surfaces under a white sky: every radiance is 1 or 0."""
+    import massrt
+    o = oracle.Scene(3)
+    o.background(massrt.BG_SOLID, 0, (1.0, 1.0, 1.0))
+    white = o.solid(1, 1, 1, 1)
+    if variant == "specular":
+        m = o.material(massrt.MAT_SPECULAR, white, 1.8)
+    elif variant == "isotrophic":
+        m = o.material(massrt.MAT_ISOTROPHIC, 0, 0.0, (1.0, 1.0, 1.0))
+    elif variant == "mix":
+        m = o.mix(0.3, o.material(massrt.MAT_LAMBERTIAN, white), o.material(massrt.MAT_SPECULAR, white, 1.8))
+    else:
+        inner = o.mix(0.5, o.material(massrt.MAT_METAL, white, 0.2), o.material(massrt.MAT_DIELECTRIC, 0, 1.5))
+        m = o.mix(0.7, inner, o.material(massrt.MAT_LAMBERTIAN, white))
+    o.add_sphere(m, (0, 0, 0), 1.0)
+    o.build_bvh()
+    o.camera(40.0, (0, 0, 4), (0, 0, 0), aspect=1.5)
+    spp = 8
+    rgb, b = o.render(24, 16, 0, spp, seed=5, threads=4)
+    rgb = rgb.reshape(-1, 3)
+    assert np.all(rgb == np.round(rgb)) and rgb.max() == spp
+    assert b.sum() > 0
