@@ -60,6 +60,7 @@ extern "C" {
 #define MRT_REF_TRIANGLE 3u /* Triangle           geom.rs:503-593 */
 #define MRT_REF_INSTANCE 4u /* Instance (of BLAS) geom.rs:403-425 */
 #define MRT_REF_MODEL 5u    /* Model (owns BLAS)  geom.rs:317-333 */
+#define MRT_REF_VOLUME 6u   /* Volume<Sphere>     geom.rs:594-660 (world level only) */
 #define MRT_REF(kind, idx) ((((uint32_t)(kind)) << MRT_REF_KIND_SHIFT) | ((uint32_t)(idx)&MRT_REF_INDEX_MASK))
 #define MRT_REF_KIND(r) (((uint32_t)(r)) >> MRT_REF_KIND_SHIFT)
 #define MRT_REF_INDEX(r) (((uint32_t)(r)) & MRT_REF_INDEX_MASK)
@@ -140,6 +141,17 @@ typedef struct {
   float color[3];
 } mrt_background;
 
+/* Volume::new(Sphere::new((), center, radius), density, albedo): a constant-
+ * density medium in a sphere (the reference's only Volume target, eve.rs:41);
+ * `material` is its Isotrophic(albedo) (material.rs:428-445). Its
+ * intersection draws from the path RNG (geom.rs:640). */
+typedef struct {
+  float center[3];
+  float radius;
+  float density;
+  uint32_t material;
+} mrt_volume;
+
 typedef struct {
   const mrt_node* nodes;
   uint32_t n_nodes;
@@ -160,6 +172,8 @@ typedef struct {
   const mrt_texture* textures;
   uint32_t n_textures;
   mrt_background background;
+  const mrt_volume* volumes;
+  uint32_t n_volumes;
 } mrt_scene_desc;
 
 /* Camera fields precomputed by Camera::new (world.rs:5-51). */
@@ -213,7 +227,7 @@ typedef struct {
   uint64_t instance_entries;
   uint64_t model_entries;
   uint64_t closest_hits;
-  uint64_t texel_taps;
+  uint64_t texel_taps;      /* bilinear taps: shading and alpha tests */
   uint64_t bounces;
   /* scheduling efficiency of the persistent k_trace (not reference quantities):
    * wave_slots = loop iterations x 64 lanes, lane_steps = box/primitive steps
@@ -245,7 +259,9 @@ int mrt_render(mrt_ctx* ctx, const mrt_render_args* args, float* accum_rgb, uint
 /* device buffers, enqueued on `hip_stream` (hipStream_t, may be NULL) */
 int mrt_render_device(mrt_ctx* ctx, const mrt_render_args* args, float* d_accum_rgb,
                       uint32_t* d_accum_bounces, void* hip_stream);
-/* rays: n x {ox,oy,oz,dx,dy,dz} host floats; out: n hits */
+/* rays: n x {ox,oy,oz,dx,dy,dz} host floats; out: n hits. Draws during the
+ * traversal (Volume, Mix alpha tests) use ray i's stream keyed
+ * (seed 0, i, sample 0xFFFFFFFE). */
 int mrt_trace_rays(mrt_ctx* ctx, const float* rays, uint32_t n, float t_min, float t_max, mrt_hit* out);
 int mrt_get_counters(mrt_ctx* ctx, mrt_counters* out);
 int mrt_reset_counters(mrt_ctx* ctx);
@@ -289,6 +305,9 @@ int mrt_builder_solid(mrt_builder* b, float r, float g, float bl, float a);
 int mrt_builder_texture_png(mrt_builder* b, const char* path, uint32_t wrap);
 int mrt_builder_texture_rgba(mrt_builder* b, const uint8_t* rgba, uint32_t w, uint32_t h, uint32_t wrap);
 int mrt_builder_material(mrt_builder* b, uint32_t kind, uint32_t surface, float param, float er, float eg, float eb);
+/* World::add(Volume::new(Sphere::new((), center, radius), density, albedo));
+ * returns the volume index */
+int mrt_builder_add_volume(mrt_builder* b, const float* center, float radius, float density, const float* albedo);
 /* Mix::new(ratio, left, right): returns the material index */
 int mrt_builder_mix(mrt_builder* b, float ratio, uint32_t left, uint32_t right);
 int mrt_builder_background(mrt_builder* b, uint32_t kind, uint32_t surface, float r, float g, float bl);

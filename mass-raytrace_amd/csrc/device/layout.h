@@ -18,6 +18,7 @@
 //   TRI    3 slots  {a.x,a.y,a.z,ab.x}        {ab.y,ab.z,tri_id,TRI} {ac.x,ac.y,ac.z,flags}
 //   INST   2 slots  {inst_id,blas_begin,blas_end,0} {0,0,0,INST}
 //   MODEL  2 slots  {model_id,blas_begin,blas_end,0} {0,0,0,MODEL}
+//   VOLUME 2 slots  {cx,cy,cz,r}              {volume_id,0,0,VOLUME}  (sphere target)
 // ab = b - a and ac = c - a are precomputed on the host with the same IEEE
 // subtraction Triangle::intersect performs (geom.rs:505-506).
 #pragma once
@@ -25,7 +26,7 @@
 
 namespace mrt {
 
-enum : uint32_t { KIND_BOX = 1, KIND_SPHERE = 2, KIND_TRI = 3, KIND_INST = 4, KIND_MODEL = 5 };
+enum : uint32_t { KIND_BOX = 1, KIND_SPHERE = 2, KIND_TRI = 3, KIND_INST = 4, KIND_MODEL = 5, KIND_VOLUME = 6 };
 // traversal-only pseudo-kind: the region being traversed has ended (path.h)
 constexpr uint32_t KIND_END = 0;
 enum : uint32_t { TRI_FLAG_ALPHA = 1u, TRI_FLAG_UV = 2u };
@@ -69,6 +70,10 @@ struct DevScene {
   // array sizes (checked only in MRT_DEBUG_BOUNDS builds) and the debug record
   uint32_t n_slots, n_tris, n_sph, n_inst, n_models, n_materials, n_textures, n_texels;
   uint32_t* dbg;  // {first failing check code, index, bound, failures}
+  const float* vol_nid;     // Volume: -1/density per volume
+  const uint32_t* vol_mat;  // Volume: its Isotrophic material
+  const float* ln_table;    // ln(m * 2^-23) for every m < 2^23 (host libm logf), when volumes exist
+  uint32_t n_vol;
   uint32_t bg_kind;
   uint32_t bg_texture;  // SkySphere texture (surface must be a texture or solid)
   uint32_t bg_surf_kind;

@@ -249,13 +249,17 @@ MRT_DEV void tri_bary(const TriShade& s, V3 point, float& a0, float& a1, float& 
 
 // Material::alpha_test of the triangle's OWN material (geom.rs:567-571,
 // material.rs:222-224,281-283): surface alpha != 0.
-MRT_DEV bool tri_alpha_pass(const DevScene& S, uint32_t id, V3 o, V3 d, float t, LocalCounters& lc) {
+template <bool RNG>
+MRT_DEV bool tri_alpha_pass(const DevScene& S, uint32_t id, V3 o, V3 d, float t, PathRng& rng, LocalCounters& lc) {
   TriShade s = load_tri(S, id);
   V3 point = o + d * t;
   float a0, a1, a2;
   tri_bary(s, point, a0, a1, a2);
   V2 uv = (s.uva * a0 + s.uvb * a1) + s.uvc * a2;
-  const GpuMaterial m = S.materials[MRT_IDX(S, s.material, S.n_materials, 4)];
+  GpuMaterial m = S.materials[MRT_IDX(S, s.material, S.n_materials, 4)];
+  // Mix::alpha_test draws to pick a side (material.rs:418-424)
+  if (RNG)
+    while (m.kind == MRT_MAT_MIX) m = S.materials[MRT_IDX(S, rng.f32() < m.param ? m.left : m.right, S.n_materials, 4)];
   // Lambertian/Metal alpha_test; Specular's forwards to its inner Lambertian
   if (m.kind != MRT_MAT_LAMBERTIAN && m.kind != MRT_MAT_METAL && m.kind != MRT_MAT_SPECULAR) return true;
   return surface_get_f(S, m, uv, lc).w != 0.0f;
@@ -294,6 +298,7 @@ struct TravIn {
   const float4* ro;        // ray origins  (xyz) of the pool
   const float4* rd;        // ray directions (xyz)
   float tmin;
+  uint4* rng = nullptr;    // the rays' RNG states (traversal draws: Volume, Mix alpha tests)
 };
 
 // Inside a BLAS, `ret` is the world record after the instance/model record
@@ -309,6 +314,7 @@ struct Trav {
   float best;
   uint32_t prim, hit_ret;  // closest hit so far: primitive (kRefNone: none) and `ret` when found
   uint4 s0, s1;  // current record (prefetched when i moves)
+  PathRng rng;   // the ray's stream, for scenes whose traversal draws (RNG variants only)
   bool done;
 #ifdef MRT_DEBUG_BOUNDS
   uint32_t steps;
@@ -430,7 +436,13 @@ MRT_DEV void trav_end(const TravIn& in, Trav& t) {
 }
 
 // Start ray `ray` of the pool (World::intersect(ray, in.tmin, tmax)).
+template <bool RNG = false>
 MRT_DEV void trav_init(const TravIn& in, Trav& t, uint32_t ray, float tmax) {
+  if (RNG) {
+    const uint4 q = in.rng[ray];
+    t.rng = PathRng{(unsigned long long)q.x | ((unsigned long long)q.y << 32),
+                    (unsigned long long)q.z | ((unsigned long long)q.w << 32)};
+  }
   t.r = world_ray(in, ray);
   t.ray = ray;
   t.i = in.S.world_begin;
@@ -460,7 +472,36 @@ MRT_DEV void trav_box(const TravIn& in, Trav& t, LocalCounters& lc) {
 // The current record is a primitive, an instance or a model. ALPHA=false is
 // the specialisation for scenes without alpha-tested triangles (the alpha
 // test's registers would otherwise cost occupancy everywhere).
-template <bool COUNT, bool ALPHA>
+// The ray's RNG state back to the pool (RNG variants, when the ray is done).
+MRT_DEV void trav_store_rng(const TravIn& in, const Trav& t) {
+  in.rng[t.ray] = make_uint4((uint32_t)t.rng.s0, (uint32_t)(t.rng.s0 >> 32), (uint32_t)t.rng.s1,
+                             (uint32_t)(t.rng.s1 >> 32));
+}
+
+// Volume::intersect with a sphere target (geom.rs:609-653): entry and exit of
+// the target over the whole line, clipped to [tmin, best], then a distance
+// f.ln() * -1/density drawn from the ray's stream; the ln is looked up
+// (S.ln_table, upload.h) for the exact value of the host libm.
+MRT_DEV bool volume_hit(const DevScene& S, const TravIn& in, Trav& t, uint4 s0, uint32_t vid, float& th) {
+  const V3 c{u2f(s0.x), u2f(s0.y), u2f(s0.z)};
+  const float rad = u2f(s0.w);
+  float te, tx;
+  if (!sphere_hit(c, rad, t.r.o, t.r.d, t.r.a, -INFINITY, INFINITY, te)) return false;
+  if (!sphere_hit(c, rad, t.r.o, t.r.d, t.r.a, te + 0.0001f, INFINITY, tx)) return false;
+  if (te < in.tmin) te = in.tmin;
+  if (tx > t.best) tx = t.best;
+  if (te >= tx) return false;
+  if (te < 0.0f) te = 0.0f;
+  const float len = sqrtf(length_squared(t.r.d));
+  const float inside = (tx - te) * len;
+  const uint32_t m = (uint32_t)(t.rng.next() >> 32) >> 9;  // the draw of f32() (mrt_rng.h)
+  const float dist = S.ln_table[MRT_IDX(S, m, 1u << 23, 14)] * S.vol_nid[MRT_IDX(S, vid, S.n_vol, 15)];
+  if (dist > inside) return false;
+  th = te + dist / len;
+  return true;
+}
+
+template <bool COUNT, bool ALPHA, bool RNG = false>
 MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
   const DevScene& S = in.S;
   const uint4 s0 = t.s0, s1 = t.s1;
@@ -475,7 +516,7 @@ MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
     V3 a{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, ab{u2f(s0.w), u2f(s1.x), u2f(s1.y)}, ac{u2f(s2.x), u2f(s2.y), u2f(s2.z)};
     float th;
     if (tri_hit(a, ab, ac, t.r.o, t.r.d, in.tmin, t.best, th)) {
-      if (!ALPHA || !(s2.w & TRI_FLAG_ALPHA) || tri_alpha_pass(S, s1.z, t.r.o, t.r.d, th, lc)) {
+      if (!ALPHA || !(s2.w & TRI_FLAG_ALPHA) || tri_alpha_pass<RNG>(S, s1.z, t.r.o, t.r.d, th, t.rng, lc)) {
         t.best = th;
         t.prim = make_ref(MRT_REF_TRIANGLE, s1.z);
         t.hit_ret = t.ret;
@@ -488,6 +529,14 @@ MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
     if (sphere_hit(V3{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, u2f(s0.w), t.r.o, t.r.d, t.r.a, in.tmin, t.best, th)) {
       t.best = th;
       t.prim = make_ref(MRT_REF_SPHERE, s1.x);
+      t.hit_ret = t.ret;
+    }
+    t.i += 2;
+  } else if (RNG && kind == KIND_VOLUME) {
+    float th;
+    if (volume_hit(S, in, t, s0, s1.x, th)) {
+      t.best = th;
+      t.prim = make_ref(MRT_REF_VOLUME, s1.x);
       t.hit_ret = t.ret;
     }
     t.i += 2;
@@ -509,17 +558,20 @@ MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
   trav_fetch(in, t);
 }
 
-// Whole traversal of pool ray `ray` (one ray per thread).
-template <bool COUNT>
-MRT_DEV Hit closest_hit(const TravIn& in, uint32_t ray, float tmax, LocalCounters& lc) {
+// Whole traversal of pool ray `ray` (one ray per thread); RNG: the
+// traversal's draws come from (and advance) `rng`.
+template <bool COUNT, bool RNG = false>
+MRT_DEV Hit closest_hit(const TravIn& in, uint32_t ray, float tmax, LocalCounters& lc, PathRng& rng) {
   Trav t;
   trav_init(in, t, ray, tmax);
+  if (RNG) t.rng = rng;
   while (!t.done) {
     if (trav_at_box(t))
       trav_box<COUNT>(in, t, lc);
     else
-      trav_prim<COUNT, true>(in, t, lc);
+      trav_prim<COUNT, true, RNG>(in, t, lc);
   }
+  if (RNG) rng = t.rng;
   return trav_hit(in, t);
 }
 
@@ -546,6 +598,14 @@ MRT_DEV Surf resolve_hit(const DevScene& S, V3 o, V3 d, const Hit& h) {
   const uint32_t pkind = h.prim >> 28, pidx = h.prim & 0x0FFFFFFFu;
   V3 outward;
   s.point = ro + rd * h.t;
+  if (pkind == MRT_REF_VOLUME) {  // geom.rs:644-651: fixed normal, front face, no uv
+    s.normal = V3{1.0f, 0.0f, 0.0f};
+    s.front_face = true;
+    s.has_uv = false;
+    s.uv = V2{0, 0};
+    s.material = S.vol_mat[MRT_IDX(S, pidx, S.n_vol, 16)];
+    return s;  // volumes are World objects: no container
+  }
   if (pkind == MRT_REF_SPHERE) {
     const uint32_t sp = MRT_IDX(S, pidx, S.n_sph, 10);
     V3 c = ld3(S.sph + (size_t)sp * 4);

@@ -171,12 +171,14 @@ struct TraceTune {
 constexpr size_t kTraceLdsMaxBytes = 64 * 1024;
 constexpr uint32_t kIdle = 0xFFFFFFFFu;  // Trav.ray of a lane without a ray
 
-// R > 1: each lane interleaves R independent rays (software ILP) — while one
-// ray's record fetch is in flight the lane steps the other, doubling the
-// memory-level parallelism a wave offers at the price of more registers.
-template <bool COUNT, bool LDS, bool ALPHA, int R>
+// RNG: the scene's traversal draws random numbers (Volume, Mix alpha tests):
+// each ray carries its path stream through the traversal and stores it back.
+// (R > 1 would interleave R rays per lane — software ILP; measured slower at
+// its 84 VGPRs, so only R = 1 is instantiated.)
+template <bool COUNT, bool LDS, bool ALPHA, bool RNG>
 __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   DevCounters* cnt, float tmin, float tmax, TraceTune tune) {
+  constexpr int R = 1;
   extern __shared__ uint4 lds_slots[];
   const uint32_t n = ctrl->active[cur];
   if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = 0;
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
     for (uint32_t k = threadIdx.x; k < S.n_slots; k += kBlock) lds_slots[k] = gslots[k];
     __syncthreads();
   }
-  const TravIn tin{S, LDS ? lds_slots : gslots, in.ro, in.rd, tmin};
+  const TravIn tin{S, LDS ? lds_slots : gslots, in.ro, in.rd, tmin, in.rng};
   LocalCounters lc;
   uint32_t seg = 0, nh = 0;
   uint32_t pool = 0, pool_end = 0;  // wave-uniform chunk [pool, pool_end)
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
       for (int q = 0; q < R; ++q) {
         if (t[q].ray == kIdle) {
           const uint32_t r = off + lane_rank(idle[q]);
-          if (r < avail) trav_init(tin, t[q], MRT_IDX(S, pool + r, n, 20), tmax);
+          if (r < avail) trav_init<RNG>(tin, t[q], MRT_IDX(S, pool + r, n, 20), tmax);
         }
         off += (uint32_t)__popcll(idle[q]);
         live |= __ballot(t[q].ray != kIdle);
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
       if (at_box) trav_box<COUNT>(tin, t[q], lc);
       // primitives wait until enough lanes are at one (or no lane is at a box)
       const bool prim_go = (__popcll(prim_mask) >= tune.prim_batch || box_mask == 0) && busy && !at_box;
-      if (prim_go) trav_prim<COUNT, ALPHA>(tin, t[q], lc);
+      if (prim_go) trav_prim<COUNT, ALPHA, RNG>(tin, t[q], lc);
       if (COUNT) {
         lc.wave_slots += lane_id() == 0 ? 64u : 0u;
         lc.lane_steps += (at_box || prim_go) ? 1u : 0u;
@@ -259,6 +261,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       if (t[q].ray != kIdle && t[q].done) {
+        if (RNG) trav_store_rng(tin, t[q]);
         const Hit h = trav_hit(tin, t[q]);
         hits[t[q].ray] = make_uint4(__float_as_uint(h.t), h.prim, h.container, 0u);
         seg += 1;
@@ -272,15 +275,24 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
 
 // Debug/bisection variant (MRT_RENDER_SIMPLE_TRACE): one ray per thread,
 // the whole traversal in closest_hit.
+template <bool RNG>
 __global__ __launch_bounds__(kBlock) void k_trace_simple(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl,
                                                          uint32_t cur, DevCounters* cnt) {
   const uint32_t n = ctrl->active[cur];
   if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = 0;
   LocalCounters lc;
   uint32_t seg = 0, nh = 0;
-  const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), in.ro, in.rd, kTmin};
+  const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), in.ro, in.rd, kTmin, in.rng};
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    Hit h = closest_hit<true>(tin, i, INFINITY, lc);
+    PathRng rng{0, 0};
+    if (RNG) {
+      const uint4 q = in.rng[i];
+      rng = PathRng{(unsigned long long)q.x | ((unsigned long long)q.y << 32),
+                    (unsigned long long)q.z | ((unsigned long long)q.w << 32)};
+    }
+    Hit h = closest_hit<true, RNG>(tin, i, INFINITY, lc, rng);
+    if (RNG)
+      in.rng[i] = make_uint4((uint32_t)rng.s0, (uint32_t)(rng.s0 >> 32), (uint32_t)rng.s1, (uint32_t)(rng.s1 >> 32));
     hits[i] = make_uint4(__float_as_uint(h.t), h.prim, h.container, 0u);
     seg += 1;
     nh += h.prim != kRefNone;
@@ -501,6 +513,8 @@ __global__ __launch_bounds__(kBlock) void k_rays_in(const float* rays, uint32_t 
   const float* r = rays + 6 * (size_t)i;
   out.ro[i] = make_float4(r[0], r[1], r[2], __uint_as_float(i));
   out.rd[i] = make_float4(r[3], r[4], r[5], __uint_as_float(0u));
+  const PathRng g = path_rng(0, i, 0xFFFFFFFEu);  // traversal draws of mrt_trace_rays (massrt.h)
+  out.rng[i] = make_uint4((uint32_t)g.s0, (uint32_t)(g.s0 >> 32), (uint32_t)g.s1, (uint32_t)(g.s1 >> 32));
 }
 
 __global__ __launch_bounds__(kBlock) void k_rays_out(DevScene S, PathBufs in, const uint4* hits, uint32_t n,
@@ -613,6 +627,7 @@ __global__ __launch_bounds__(kBlock) void k_max_u32(const uint32_t* v, uint32_t 
 
 // Camera::albedo_normal for pixel p (one ray, no jitter). The rays go through
 // ray_ro/ray_rd so that the traversal can re-read them (TravIn).
+template <bool RNG>
 __global__ __launch_bounds__(kBlock) void k_prepass(DevScene S, DevCamera cam, uint32_t W, uint32_t H,
                                                     unsigned long long seed, float4* ray_ro, float4* ray_rd,
                                                     float* albedo, float* normal) {
@@ -626,7 +641,7 @@ __global__ __launch_bounds__(kBlock) void k_prepass(DevScene S, DevCamera cam, u
   ray_rd[p] = make_float4(d.x, d.y, d.z, 0.0f);
   const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), ray_ro, ray_rd, kTmin};
   LocalCounters lc;
-  const Hit h = closest_hit<false>(tin, p, INFINITY, lc);
+  const Hit h = closest_hit<false, RNG>(tin, p, INFINITY, lc, rng);
   V3 a{0.0f, 0.0f, 0.0f}, n{0.0f, 0.0f, 0.0f};
   if (h.prim != kRefNone) {
     Surf s = resolve_hit(S, o, d, h);
@@ -791,9 +806,9 @@ struct mrt_ctx {
   DevCounters* d_cnt = nullptr;
   uint32_t* dbg = nullptr;  // MRT_DEBUG_BOUNDS record (4 words)
   uint32_t trace_grid = 1024;  // k_trace_simple workgroups
-  int rays_per_lane = 1;       // k_trace R (MRT_TRACE_RAYS_PER_LANE)
   std::map<std::pair<const void*, size_t>, uint32_t> grids;  // persistent grid per (kernel, LDS bytes)
   bool scene_alpha = true;  // the scene has alpha-tested triangles
+  bool scene_rng = false;   // the traversal draws random numbers (Volume, Mix alpha tests)
   TraceTune tune;
   // k_render: per-lane current world ray; event pair timing one launch
   float4* slot_ro = nullptr;
@@ -884,27 +899,27 @@ uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem) {
   return g;
 }
 
-template <bool LDS, bool ALPHA, int R>
+template <bool LDS, bool ALPHA, bool RNG>
 void launch_trace_r(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
                     float tmin, float tmax) {
   const size_t smem = LDS ? (size_t)c->S.n_slots * 16 : 0;
-  const void* f = count ? (const void*)k_trace<true, LDS, ALPHA, R> : (const void*)k_trace<false, LDS, ALPHA, R>;
+  const void* f = count ? (const void*)k_trace<true, LDS, ALPHA, RNG> : (const void*)k_trace<false, LDS, ALPHA, RNG>;
   const uint32_t grid = persistent_grid(c, f, smem);
   if (count)
-    hipLaunchKernelGGL((k_trace<true, LDS, ALPHA, R>), dim3(grid), dim3(kBlock), smem, st, c->S, in, q.hits,
+    hipLaunchKernelGGL((k_trace<true, LDS, ALPHA, RNG>), dim3(grid), dim3(kBlock), smem, st, c->S, in, q.hits,
                        q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
   else
-    hipLaunchKernelGGL((k_trace<false, LDS, ALPHA, R>), dim3(grid), dim3(kBlock), smem, st, c->S, in, q.hits,
+    hipLaunchKernelGGL((k_trace<false, LDS, ALPHA, RNG>), dim3(grid), dim3(kBlock), smem, st, c->S, in, q.hits,
                        q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
 }
 
 template <bool LDS, bool ALPHA>
 void launch_trace_v(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
                     float tmin, float tmax) {
-  if (c->rays_per_lane == 2)
-    launch_trace_r<LDS, ALPHA, 2>(c, st, q, in, cur, count, tmin, tmax);
+  if (c->scene_rng)
+    launch_trace_r<LDS, ALPHA, true>(c, st, q, in, cur, count, tmin, tmax);
   else
-    launch_trace_r<LDS, ALPHA, 1>(c, st, q, in, cur, count, tmin, tmax);
+    launch_trace_r<LDS, ALPHA, false>(c, st, q, in, cur, count, tmin, tmax);
 }
 
 void launch_trace(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
@@ -1079,6 +1094,8 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
   // results slab <= kResultsMax samples (16 B each); pool <= c->pool_paths
   uint32_t spp_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(a->spp_count, kResultsMax / n_pix));
   if ((a->flags & MRT_RENDER_FUSED) && !(a->flags & MRT_RENDER_SIMPLE_TRACE)) {
+    if (c->scene_rng)
+      throw ApiError{MRT_ERR_INVALID, "MRT_RENDER_FUSED does not support scenes whose traversal draws (Volume, Mix alpha)"};
     render_fused(c, a, pl.first, n_pix, spp_chunk, d_rgb, d_b, st);
     return;
   }
@@ -1151,8 +1168,12 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
             HIP_CHECK(hipEventRecord(m[0], q.stream));
           }
           if (a->flags & MRT_RENDER_SIMPLE_TRACE)
-            hipLaunchKernelGGL(k_trace_simple, dim3(c->trace_grid), dim3(kBlock), 0, q.stream, c->S, q.bufs[cur],
-                               q.hits, q.ctrl, cur, c->d_cnt);
+            if (c->scene_rng)
+              hipLaunchKernelGGL(k_trace_simple<true>, dim3(c->trace_grid), dim3(kBlock), 0, q.stream, c->S,
+                                 q.bufs[cur], q.hits, q.ctrl, cur, c->d_cnt);
+            else
+              hipLaunchKernelGGL(k_trace_simple<false>, dim3(c->trace_grid), dim3(kBlock), 0, q.stream, c->S,
+                                 q.bufs[cur], q.hits, q.ctrl, cur, c->d_cnt);
           else
             launch_trace(c, q.stream, q, q.bufs[cur], cur, count, kTmin, INFINITY);
           HIP_CHECK(hipGetLastError());
@@ -1270,7 +1291,6 @@ int mrt_create(int device, mrt_ctx** out) {
     if (const char* e = getenv("MRT_TRACE_BOX_MIN")) c->tune.box_min = (uint32_t)std::max(1, std::min(65, atoi(e)));
     if (const char* e = getenv("MRT_SHADE_BATCH")) c->tune.shade_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_POOL_PATHS")) c->pool_paths = (size_t)std::max(1 << 16, std::min(1 << 28, atoi(e)));
-    if (const char* e = getenv("MRT_TRACE_RAYS_PER_LANE")) c->rays_per_lane = atoi(e) == 2 ? 2 : 1;
   });
   if (rc != MRT_OK) {
     g_last_error = c->err;
@@ -1334,7 +1354,10 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
            o_fwd = sec(hs.inst_fwd.size() * 4), o_imat = sec(hs.inst_mat.size() * 4),
            o_mmat = sec(hs.model_mat.size() * 4), o_sph = sec(hs.sph.size() * 4), o_smat = sec(hs.sph_mat.size() * 4),
            o_tri = sec(hs.tri_shade.size() * 4), o_mat = sec(hs.materials.size() * sizeof(GpuMaterial)),
-           o_tex = sec(hs.textures.size() * sizeof(GpuTexture)), o_texel = sec(hs.texels.size() * 4);
+           o_tex = sec(hs.textures.size() * sizeof(GpuTexture)), o_texel = sec(hs.texels.size() * 4),
+           o_vnid = sec(hs.vol_nid.size() * 4), o_vmat = sec(hs.vol_mat.size() * 4);
+    const std::vector<float>& ln_table = hs.ln_table;
+    const size_t o_ln = sec(ln_table.size() * 4);
     if (c->scene_mem) HIP_CHECK(hipFree(c->scene_mem));
     c->scene_mem = nullptr;
     c->has_scene = false;
@@ -1344,6 +1367,9 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
       if (bytes) HIP_CHECK(hipMemcpy(base + o, src, bytes, hipMemcpyHostToDevice));
     };
     up(o_slots, hs.slots.data(), hs.slots.size() * 4);
+    up(o_vnid, hs.vol_nid.data(), hs.vol_nid.size() * 4);
+    up(o_vmat, hs.vol_mat.data(), hs.vol_mat.size() * 4);
+    up(o_ln, ln_table.data(), ln_table.size() * 4);
     up(o_inv, hs.inst_inv.data(), hs.inst_inv.size() * 4);
     up(o_fwd, hs.inst_fwd.data(), hs.inst_fwd.size() * 4);
     up(o_imat, hs.inst_mat.data(), hs.inst_mat.size() * 4);
@@ -1369,6 +1395,10 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     S.textures = (const GpuTexture*)(base + o_tex);
     S.texels = (const uint32_t*)(base + o_texel);
     S.fast_ok = hs.fast_ok;
+    S.vol_nid = (const float*)(base + o_vnid);
+    S.vol_mat = (const uint32_t*)(base + o_vmat);
+    S.ln_table = ln_table.empty() ? nullptr : (const float*)(base + o_ln);
+    S.n_vol = (uint32_t)hs.vol_nid.size();
     S.n_slots = (uint32_t)(hs.slots.size() / 4);
     S.n_tris = (uint32_t)(hs.tri_shade.size() / (kTriShadeQuads * 4));
     S.n_sph = (uint32_t)hs.sph_mat.size();
@@ -1388,6 +1418,7 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     const char* no_lds = getenv("MRT_TRACE_LDS");
     c->trace_lds = lds_bytes <= kTraceLdsMaxBytes && !(no_lds && no_lds[0] == '0');
     c->scene_alpha = hs.has_alpha;
+    c->scene_rng = hs.trav_rng;
     c->has_scene = true;
   });
 }
@@ -1596,8 +1627,12 @@ int mrt_prepass_device(mrt_ctx* c, uint32_t W, uint32_t H, uint64_t seed, float*
     wait_queues(c, st);
     const uint32_t n = W * H;
     ensure_slots(c, n);  // the pre-pass rays
-    hipLaunchKernelGGL(k_prepass, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c->S, c->cam, W, H,
-                       (unsigned long long)seed, c->slot_ro, c->slot_rd, d_albedo, d_normal);
+    if (c->scene_rng)
+      hipLaunchKernelGGL(k_prepass<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c->S, c->cam, W, H,
+                         (unsigned long long)seed, c->slot_ro, c->slot_rd, d_albedo, d_normal);
+    else
+      hipLaunchKernelGGL(k_prepass<false>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c->S, c->cam, W, H,
+                         (unsigned long long)seed, c->slot_ro, c->slot_rd, d_albedo, d_normal);
     HIP_CHECK(hipGetLastError());
   });
 }

@@ -58,6 +58,16 @@ struct Emitter {
         s.n_prim_records++;
         return true;
       }
+      case MRT_REF_VOLUME: {
+        if (idx >= d.n_volumes) return fail("volume index out of range");
+        if (in_blas) return fail("a Volume must be a World object (not inside a model)");
+        const mrt_volume& v = d.volumes[idx];
+        push_slot(fbits(v.center[0]), fbits(v.center[1]), fbits(v.center[2]), fbits(v.radius));
+        push_slot(idx, 0, 0, KIND_VOLUME);
+        s.n_prim_records++;
+        s.trav_rng = true;
+        return true;
+      }
       case MRT_REF_INSTANCE:
       case MRT_REF_MODEL: {
         if (in_blas) return fail("instances/models cannot be nested inside a BLAS");
@@ -233,6 +243,17 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
     memcpy(&q[25], &flags, 4);
     s.tri_shade.insert(s.tri_shade.end(), q, q + 28);
   }
+  // volumes (geom.rs:602-607: neg_inv_density = -1.0 / density)
+  for (uint32_t i = 0; i < d.n_volumes; ++i) {
+    const mrt_volume& v = d.volumes[i];
+    if (!check_mat(v.material, false)) return (err = "volume material out of range", false);
+    s.vol_nid.push_back(-1.0f / v.density);
+    s.vol_mat.push_back(v.material);
+  }
+  if (d.n_volumes) {
+    s.ln_table.resize((size_t)1 << 23);
+    for (uint32_t m = 0; m < (1u << 23); ++m) s.ln_table[m] = logf((float)m * 0x1p-23f);
+  }
   // instances / models
   for (uint32_t i = 0; i < d.n_instances; ++i) {
     const mrt_instance& in = d.instances[i];
@@ -275,9 +296,7 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
     s.slots[4 * p.first + 1] = it->second.first;
     s.slots[4 * p.first + 2] = it->second.second;
   }
-  if (e.mix_alpha)
-    return (err = "a Mix material on a triangle with uvs (its alpha test draws random numbers during traversal) "
-                  "is not supported yet", false);
+  if (e.mix_alpha) s.trav_rng = true;
   if (s.slots.size() / 4 >= 0x80000000ull) return (err = "scene too large (record stream >= 2^31 slots)", false);
   return true;
 }

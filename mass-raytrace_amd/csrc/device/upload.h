@@ -21,6 +21,14 @@ struct HostScene {
   std::vector<uint32_t> texels;
   uint32_t fast_ok = 1;
   bool has_alpha = false;  // some triangle carries TRI_FLAG_ALPHA
+  bool trav_rng = false;   // the traversal draws random numbers (Volume, Mix alpha tests)
+  std::vector<float> vol_nid;
+  std::vector<uint32_t> vol_mat;
+  // Volume draws f = m * 2^-23 (m < 2^23, mrt_rng.h) and takes f.ln()
+  // (geom.rs:640): the device looks up the host libm logf of every such f
+  // instead of computing it, so the distance is the reference's to the bit
+  // (32 MiB, built only when the scene has volumes).
+  std::vector<float> ln_table;
   uint32_t bg_kind = 0, bg_texture = 0, bg_surf_kind = 0;
   float bg_color[4] = {0, 0, 0, 0};
   // statistics

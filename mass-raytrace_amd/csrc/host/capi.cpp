@@ -173,6 +173,13 @@ int mrt_builder_add_sphere(mrt_builder* b, uint32_t material, float cx, float cy
   });
 }
 
+int mrt_builder_add_volume(mrt_builder* b, const float* center, float radius, float density, const float* albedo) {
+  return guard(b, [&] {
+    if (!center || !albedo) throw Error(MRT_ERR_INVALID, "null argument");
+    return (int)b->world->add(VolumeDesc{v3p(center), radius, density, v3p(albedo)});
+  });
+}
+
 int mrt_builder_add_triangle(mrt_builder* b, uint32_t material, const float* abc) {
   return guard(b, [&] {
     if (!abc) throw Error(MRT_ERR_INVALID, "null vertices");

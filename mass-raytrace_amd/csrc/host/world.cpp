@@ -244,6 +244,19 @@ void World::add(const SphereDesc& s) {
   objects_.push_back(Item{MRT_REF(MRT_REF_SPHERE, idx), BoundingBox{s.center - fill3(r), s.center + fill3(r)}});
 }
 
+uint32_t World::add(const VolumeDesc& v) {
+  uint32_t idx = (uint32_t)volumes_.size();
+  mrt_volume d;
+  put3(d.center, v.center);
+  d.radius = v.radius;
+  d.density = v.density;
+  d.material = intern_material(Isotrophic(v.albedo));
+  volumes_.push_back(d);
+  float r = fabsf(v.radius);  // Volume::bounding_box = the target's (geom.rs:656-658)
+  objects_.push_back(Item{MRT_REF(MRT_REF_VOLUME, idx), BoundingBox{v.center - fill3(r), v.center + fill3(r)}});
+  return idx;
+}
+
 static mrt_triangle to_abi(const Triangle& t, uint32_t material) {
   mrt_triangle d{};
   put3(d.a, t.vertex_a);
@@ -346,6 +359,8 @@ const mrt_scene_desc& World::desc() {
   desc_.textures = textures_.data();
   desc_.n_textures = (uint32_t)textures_.size();
   desc_.background = bg;
+  desc_.volumes = volumes_.data();
+  desc_.n_volumes = (uint32_t)volumes_.size();
   return desc_;
 }
 

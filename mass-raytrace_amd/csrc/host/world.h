@@ -227,6 +227,14 @@ struct SphereDesc {
 };
 inline SphereDesc Sphere(Material m, V3 center, float radius) { return SphereDesc{center, radius, std::move(m)}; }
 
+// Volume::new(Sphere::new((), center, radius), density, albedo) (geom.rs:594-607)
+struct VolumeDesc {
+  V3 center;
+  float radius;
+  float density;
+  V3 albedo;
+};
+
 struct Camera {  // world.rs:5-51
   V3 origin, lower_left_corner, horizontal, vertical, u, v;
   float lens_radius = 0;
@@ -248,6 +256,7 @@ class World {
   void add(const Triangle& t);
   void add(const InstanceDesc& inst);
   void add(Model& m);  // World::add(model)
+  uint32_t add(const VolumeDesc& v);
   // Model::new / Model::with_material: builds the BLAS now (consumes RNG)
   Model model(std::vector<Triangle> triangles);
   Model model_with_material(Material m, std::vector<Triangle> triangles);
@@ -273,6 +282,7 @@ class World {
   std::vector<mrt_triangle> triangles_;
   std::vector<mrt_instance> instances_;
   std::vector<mrt_model> models_;
+  std::vector<mrt_volume> volumes_;
   std::vector<mrt_material> materials_;
   std::vector<mrt_surface> surfaces_;
   std::vector<mrt_texture> textures_;

@@ -27,7 +27,7 @@ REPO = _HERE.parent.parent
 
 # ---- constants (massrt.h) --------------------------------------------------
 ABI_VERSION = 2  # MRT_ABI_VERSION this binding was written for
-REF_NONE, REF_NODE, REF_SPHERE, REF_TRIANGLE, REF_INSTANCE, REF_MODEL = range(6)
+REF_NONE, REF_NODE, REF_SPHERE, REF_TRIANGLE, REF_INSTANCE, REF_MODEL, REF_VOLUME = range(7)
 MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_SPECULAR, MAT_ISOTROPHIC, MAT_MIX = range(8)
 WRAP_MIRROR, WRAP_REPEAT, WRAP_CLAMP = range(3)
 BG_SOLID, BG_SKY, BG_SKYSPHERE = range(3)
@@ -103,6 +103,7 @@ class MrtSceneDesc(C.Structure):
         ("surfaces", C.POINTER(MrtSurface)), ("n_surfaces", C.c_uint32),
         ("textures", C.POINTER(MrtTexture)), ("n_textures", C.c_uint32),
         ("background", MrtBackground),
+        ("volumes", C.c_void_p), ("n_volumes", C.c_uint32),
     ]
 
 
@@ -159,7 +160,7 @@ EXPORTED_SYMBOLS = [
     "mrt_get_counters", "mrt_reset_counters", "mrt_scene_device_bytes", "mrt_get_kernel_stats",
     "mrt_reset_kernel_stats", "mrt_selftest_division", "mrt_selftest_slab", "mrt_debug_status", "mrt_debug_build",
     "mrt_builder_new", "mrt_builder_free", "mrt_builder_builtin", "mrt_builder_rand_f32", "mrt_builder_solid",
-    "mrt_builder_texture_png", "mrt_builder_texture_rgba", "mrt_builder_material", "mrt_builder_mix",
+    "mrt_builder_texture_png", "mrt_builder_texture_rgba", "mrt_builder_material", "mrt_builder_mix", "mrt_builder_add_volume",
     "mrt_builder_background",
     "mrt_builder_add_sphere", "mrt_builder_add_triangle", "mrt_builder_model", "mrt_builder_model_from_ply",
     "mrt_builder_add_instance", "mrt_builder_camera", "mrt_builder_build_bvh", "mrt_builder_desc",
@@ -212,6 +213,7 @@ def lib() -> C.CDLL:
         "mrt_builder_material": (I, [P, U32, U32, F, F, F, F]),
         "mrt_builder_background": (I, [P, U32, U32, F, F, F]),
         "mrt_builder_mix": (I, [P, F, U32, U32]),
+        "mrt_builder_add_volume": (I, [P, fp, F, F, fp]),
         "mrt_builder_add_sphere": (I, [P, U32, F, F, F, F]),
         "mrt_builder_add_triangle": (I, [P, U32, fp]),
         "mrt_builder_model": (I, [P, U32, U32, fp, U32, I, I]),
@@ -309,6 +311,11 @@ class Builder:
 
     def add_sphere(self, material, center, radius):
         _check_builder(lib().mrt_builder_add_sphere(self.h, material, *[float(c) for c in center], radius))
+
+    def add_volume(self, center, radius, density, albedo) -> int:
+        """World::add(Volume::new(Sphere(center, radius), density, albedo)) (geom.rs:595-653)."""
+        return _check_builder(lib().mrt_builder_add_volume(self.h, _fptr(_f3(center)), float(radius), float(density),
+                                                           _fptr(_f3(albedo))))
 
     def add_triangle(self, material, abc):
         a = np.ascontiguousarray(np.asarray(abc, dtype=np.float32).reshape(9))

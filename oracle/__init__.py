@@ -47,6 +47,7 @@ def lib() -> C.CDLL:
         "orc_background": (I, [P, U32, U32, F, F, F]),
         "orc_mix": (I, [P, F, U32, U32]),
         "orc_add_sphere": (I, [P, U32, F, F, F, F]),
+        "orc_add_volume": (I, [P, F, F, F, F, F, F, F, F]),
         "orc_add_triangle": (I, [P, U32, fp]),
         "orc_model": (I, [P, U32, U32, fp, U32, I, I]),
         "orc_model_from_ply": (I, [P, C.c_char_p, U32, U32, I]),
@@ -177,6 +178,11 @@ class Scene:
 
     def add_sphere(self, material, center, radius):
         self._chk(lib().orc_add_sphere(self.h, material, *[float(c) for c in center], radius))
+
+    def add_volume(self, center, radius, density, albedo):
+        """geom.rs:595 Volume(Sphere(center, radius), density, albedo)."""
+        self._chk(lib().orc_add_volume(self.h, *[float(c) for c in center], float(radius), float(density),
+                                       *[float(c) for c in albedo]))
 
     def add_triangle(self, material, abc):
         a = np.ascontiguousarray(np.asarray(abc, dtype=np.float32).reshape(9))

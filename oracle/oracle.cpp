@@ -451,7 +451,7 @@ struct SkySphere : Background {  // material.rs:65-89
 };
 
 // ---------------------------------------------------------------- geom.rs
-enum { REF_NONE = 0, REF_NODE = 1, REF_SPHERE = 2, REF_TRI = 3, REF_INST = 4, REF_MODEL = 5 };
+enum { REF_NONE = 0, REF_NODE = 1, REF_SPHERE = 2, REF_TRI = 3, REF_INST = 4, REF_MODEL = 5, REF_VOLUME = 6 };
 static inline uint32_t mkref(uint32_t k, uint32_t i) { return (k << 28) | i; }
 
 struct BoundingBox {  // geom.rs:207-273
@@ -503,8 +503,8 @@ struct Sphere : Intersect {  // geom.rs:40-101
   float radius;
   std::shared_ptr<Material> material;
   uint32_t id;
-  bool intersect(const Ray& ray, float t_min, float t_max, Hit& out, Ctx& c) const override {
-    c.cnt.sphere_tests++;
+  // the root search of geom.rs:48-66 (shared with Volume's target)
+  static bool root_of(V3 center, float radius, const Ray& ray, float t_min, float t_max, float& root) {
     V3 oc = ray.origin - center;
     float a = length_squared(ray.direction);
     float half_b = dot(oc, ray.direction);
@@ -512,11 +512,17 @@ struct Sphere : Intersect {  // geom.rs:40-101
     float disc = (half_b * half_b) - (a * cc);
     if (disc < 0.0f) return false;
     float sq = sqrtf(disc);
-    float root = (-half_b - sq) / a;
+    root = (-half_b - sq) / a;
     if (root < t_min || t_max < root) {
       root = (-half_b + sq) / a;
       if (root < t_min || t_max < root) return false;
     }
+    return true;
+  }
+  bool intersect(const Ray& ray, float t_min, float t_max, Hit& out, Ctx& c) const override {
+    c.cnt.sphere_tests++;
+    float root;
+    if (!root_of(center, radius, ray, t_min, t_max, root)) return false;
     Hit h;
     h.point = ray.at(root);
     V3 n = (h.point - center) / radius;
@@ -533,6 +539,47 @@ struct Sphere : Intersect {  // geom.rs:40-101
     return {center - fill(r), center + fill(r)};
   }
   void preorder(PreorderSink& s) const override { s.push(REF_SPHERE, id, nullptr); }
+};
+
+// geom.rs:595-653 — constant-density medium bounded by a sphere target
+// (the form eve.rs:41 builds). The target's two intersections are not
+// counted as sphere tests; the free-path draw is one f32 from the ray's
+// stream, so Ctx::rng must be set (trace_rays keys it per ray).
+struct Volume : Intersect {
+  V3 center;
+  float radius;
+  float neg_inv_density;
+  std::shared_ptr<Material> material;  // Isotrophic(albedo)
+  uint32_t id;
+  bool intersect(const Ray& ray, float t_min, float t_max, Hit& out, Ctx& c) const override {
+    float te, tx;
+    if (!Sphere::root_of(center, radius, ray, -INFINITY, INFINITY, te)) return false;
+    if (!Sphere::root_of(center, radius, ray, te + 0.0001f, INFINITY, tx)) return false;
+    if (te < t_min) te = t_min;
+    if (tx > t_max) tx = t_max;
+    if (te >= tx) return false;
+    if (te < 0.0f) te = 0.0f;
+    float len = sqrtf(length_squared(ray.direction));
+    float inside = (tx - te) * len;
+    float dist = logf(c.rand()) * neg_inv_density;
+    if (dist > inside) return false;
+    float t = te + dist / len;
+    Hit h;
+    h.point = ray.at(t);
+    h.normal = V3{1.0f, 0.0f, 0.0f};
+    h.front_face = true;
+    h.t = t;
+    h.has_uv = false;
+    h.material = material.get();
+    h.prim = mkref(REF_VOLUME, id);
+    out = h;
+    return true;
+  }
+  BoundingBox bounding_box() const override {
+    float r = fabsf(radius);
+    return {center - fill(r), center + fill(r)};
+  }
+  void preorder(PreorderSink& s) const override { s.push(REF_VOLUME, id, nullptr); }
 };
 
 struct Triangle : Intersect {  // geom.rs:427-593
@@ -778,7 +825,7 @@ struct orc_scene {
   std::vector<std::shared_ptr<Material>> materials;
   std::vector<std::shared_ptr<BvhNode>> blas;  // every Model's BvhNode in creation order
   std::vector<std::shared_ptr<Material>> model_override;
-  uint32_t n_spheres = 0, n_tris = 0, n_inst = 0, n_models = 0;
+  uint32_t n_spheres = 0, n_tris = 0, n_inst = 0, n_models = 0, n_volumes = 0;
   std::vector<Model*> world_models;  // models added to the world
   Counters counters;
   std::mutex mu;
@@ -1349,6 +1396,17 @@ int orc_add_sphere(orc_scene* s, uint32_t m, float cx, float cy, float cz, float
     return 0;
   });
 }
+int orc_add_volume(orc_scene* s, float cx, float cy, float cz, float r, float density, float ar, float ag,
+                   float ab) {
+  return guard([&] {
+    auto* v = new Volume();
+    v->center = V3{cx, cy, cz}, v->radius = r, v->neg_inv_density = -1.0f / density;
+    v->material = std::make_shared<Isotrophic>(V3{ar, ag, ab});
+    v->id = s->n_volumes++;
+    s->world.objects.push_back(Obj(v));
+    return 0;
+  });
+}
 int orc_add_triangle(orc_scene* s, uint32_t m, const float* abc) {
   return guard([&] {
     s->world.objects.push_back(Obj(new_tri(s, mat(s, m), v3p(abc), v3p(abc + 3), v3p(abc + 6))));
@@ -1429,6 +1487,8 @@ int orc_trace_rays(orc_scene* s, const float* rays, uint32_t n, float tmin, floa
     Ctx c;
     for (uint32_t i = 0; i < n; ++i) {
       Ray r{v3p(rays + 6 * (size_t)i), v3p(rays + 6 * (size_t)i + 3)};
+      PathRng rng(0, i, 0xFFFFFFFEu);  // traversal draws (Volume, Mix alpha): massrt.h mrt_trace_rays
+      c.rng = &rng;
       Hit h;
       if (s->world.intersect(r, tmin, tmax, h, c)) {
         out[i] = orc_hit{h.prim, h.container, h.t, h.front_face ? 1u : 0u};

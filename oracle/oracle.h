@@ -51,6 +51,9 @@ int orc_material(orc_scene* s, uint32_t kind, uint32_t surface, float param, flo
 int orc_mix(orc_scene* s, float ratio, uint32_t left, uint32_t right);
 int orc_background(orc_scene* s, uint32_t kind, uint32_t surface, float r, float g, float b);
 int orc_add_sphere(orc_scene* s, uint32_t material, float cx, float cy, float cz, float radius);
+// geom.rs:595-653 Volume over a Sphere target with an Isotrophic(albedo) material
+int orc_add_volume(orc_scene* s, float cx, float cy, float cz, float radius, float density, float ar, float ag,
+                   float ab);
 int orc_add_triangle(orc_scene* s, uint32_t material, const float* abc);
 int orc_model(orc_scene* s, uint32_t tri_material, uint32_t override_material, const float* tris, uint32_t n,
               int with_shading, int add_to_world);

@@ -422,3 +422,48 @@ def test_extended_materials_parity(ctx):
     ga, gn = ctx.prepass(64, 36, seed=2)
     oa, on = o.prepass(64, 36, seed=2)
     assert np.array_equal(gn, on) and np.array_equal(ga, oa)
+
+
+def test_volumes_and_mix_alpha_parity(ctx):
+    """Traversal draws (massrt.h mrt_trace_rays): Volume free paths
+    (geom.rs:595-653) and the Mix alpha pick on cut-out triangles
+    (material.rs:391-426 alpha) come from the ray's own stream, interleaved
+    with the scatter draws exactly as in the reference's thread-local rand."""
+    rng = np.random.default_rng(11)
+    tex, tris = _alpha_plane(rng)
+    tex2 = tex.copy()
+    tex2[..., 3] = np.where(rng.random((16, 24)) < 0.5, 0, 255)
+
+    def scene(x):
+        x.background(massrt.BG_SKY)
+        s1, s2 = x.texture_rgba(tex, massrt.WRAP_REPEAT), x.texture_rgba(tex2, massrt.WRAP_REPEAT)
+        mix = x.mix(0.4, x.material(massrt.MAT_LAMBERTIAN, s1), x.material(massrt.MAT_METAL, s2, 0.2))
+        x.model(mix, tris, add_to_world=True, shading=True)
+        x.add_sphere(x.material(massrt.MAT_LAMBERTIAN, x.solid(0.5, 0.5, 0.5, 1)), (0, -101, 0), 100.0)
+        x.add_volume((0.4, 0.0, 0.8), 0.7, 1.2, (0.6, 0.7, 0.8))
+        x.add_volume((-1.2, 0.3, 1.0), 0.5, 20.0, (0.9, 0.3, 0.2))
+        x.add_sphere(x.material(massrt.MAT_DIELECTRIC, 0, 1.5), (1.3, 0.2, 1.2), 0.4)
+        x.add_volume((1.3, 0.2, 1.2), 0.3, 3.0, (0.9, 0.9, 0.9))  # medium inside the glass ball
+        x.build_bvh()
+        x.camera(45.0, (0.3, 0.8, 6), (0, 0, 0), aspect=ASPECT)
+    b, o = build_both(scene)
+    ctx.upload(b)
+    _, cam = b.desc()
+    rays = camera_rays(cam, 20_000, 5)
+    g, r = ctx.trace_rays(rays), o.trace_rays(rays)
+    assert np.array_equal(g, r)
+    assert np.any(r[:, 0] >> 28 == massrt.REF_VOLUME)
+    ctx.reset_counters()
+    o.reset_counters()
+    rgb, bo = ctx.render(64, 36, 0, 4, seed=13, counters=True)
+    orgb, obo = o.render(64, 36, 0, 4, seed=13)
+    assert np.array_equal(bo, obo)
+    assert rel_l2(rgb, orgb) <= RTOL
+    gc, oc = ctx.counters(), o.counters()
+    oc["texel_taps"] += oc["alpha_taps"]  # the device counts alpha-test taps as texel taps
+    for k in massrt.COUNTER_FIELDS:
+        assert gc[k] == oc[k], (k, gc[k], oc[k])
+    assert oc["alpha_taps"] > 0
+    ga, gn = ctx.prepass(64, 36, seed=2)
+    oa, on = o.prepass(64, 36, seed=2)
+    assert np.array_equal(gn, on) and np.array_equal(ga, oa)

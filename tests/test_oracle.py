@@ -161,3 +161,40 @@ def test_extended_materials_furnace(variant):
     rgb = rgb.reshape(-1, 3)
     assert np.all(rgb == np.round(rgb)) and rgb.max() == spp
     assert b.sum() > 0
+
+
+def test_volume_free_path_statistics():
+    """Volume (geom.rs:595-653): a ray through the centre of a unit sphere of
+    density d scatters with probability 1 - exp(-2d); hits lie inside the
+    sphere with normal-free front_face = 1; the draw is keyed per ray, so a
+    second trace is identical."""
+    o = oracle.Scene(1)
+    o.add_volume((0, 0, -5), 1.0, 0.5, (0.5, 0.5, 0.5))
+    o.build_bvh()
+    n = 20_000
+    rays = np.zeros((n, 6), np.float32)
+    rays[:, 5] = -2.0  # unnormalised direction: distances scale by |d|
+    h = o.trace_rays(rays, 0.001, INF)
+    hit = h[:, 0] != 0
+    assert np.all(h[hit, 0] == (massrt.REF_VOLUME << 28)) and np.all(h[hit, 3] == 1)
+    assert abs(hit.mean() - (1 - np.exp(-1.0))) < 0.015
+    t = h[hit, 2].view(np.float32)
+    assert t.min() >= 2.0 and t.max() <= 3.0  # z in [-6, -4]
+    assert np.array_equal(o.trace_rays(rays, 0.001, INF), h)
+    # clipped by t_max: nothing past it
+    h2 = o.trace_rays(rays, 0.001, 2.25)
+    assert np.all(h2[h2[:, 0] != 0, 2].view(np.float32) <= 2.25)
+
+
+def test_volume_furnace():
+    """A white Isotrophic medium under a white sky: every sample is 1 or 0."""
+    o = oracle.Scene(3)
+    o.background(massrt.BG_SOLID, 0, (1.0, 1.0, 1.0))
+    o.add_volume((0, 0, 0), 1.0, 2.0, (1.0, 1.0, 1.0))
+    o.build_bvh()
+    o.camera(40.0, (0, 0, 4), (0, 0, 0), aspect=1.5)
+    spp = 8
+    rgb, b = o.render(24, 16, 0, spp, seed=5, threads=4)
+    rgb = rgb.reshape(-1, 3)
+    assert np.all(rgb == np.round(rgb)) and rgb.max() == spp
+    assert b.max() > spp  # multiple scattering inside the medium
