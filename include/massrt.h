@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 2
+#define MRT_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 #define MRT_OK 0
@@ -116,12 +116,24 @@ typedef struct {
   uint32_t left, right; /* Mix only */
 } mrt_material;
 
-#define MRT_SURF_SOLID 0u   /* SolidColor  texture.rs:179-194 */
-#define MRT_SURF_TEXTURE 1u /* Texture     texture.rs:117-149 */
+#define MRT_SURF_SOLID 0u    /* SolidColor         texture.rs:179-194 */
+#define MRT_SURF_TEXTURE 1u  /* Texture            texture.rs:117-149 */
+#define MRT_SURF_YCBCR 2u    /* YCbCrTexture       texture.rs:207-250: texture = luma, a = chroma texture */
+#define MRT_SURF_BLEND 3u    /* TextureBlend       texture.rs:303-334: mode, a = left, b = right surface */
+#define MRT_SURF_FALLBACK 4u /* SolidColorFallback texture.rs:336-357: color, a = surface */
+/* BlendMode (texture.rs:252-267) */
+#define MRT_BLEND_LIGHTEN 0u
+#define MRT_BLEND_DARKEN 1u
+#define MRT_BLEND_ADDITION 2u
+#define MRT_BLEND_SUBTRACTION 3u
+/* Composite surfaces (BLEND, FALLBACK) reference surfaces with lower
+ * indices, so the table is acyclic; evaluating one may hold at most 4
+ * operands at once (e.g. Blend(Texture, YCbCr) holds 3). */
 typedef struct {
   uint32_t kind;
   uint32_t texture;
   float color[4];
+  uint32_t a, b, mode;
 } mrt_surface;
 
 #define MRT_WRAP_MIRROR 0u /* unimplemented in the reference (texture.rs:280-282) */
@@ -135,10 +147,15 @@ typedef struct {
 #define MRT_BG_SOLID 0u     /* SolidBackground material.rs:39-53 */
 #define MRT_BG_SKY 1u       /* SkyBackground   material.rs:55-63 */
 #define MRT_BG_SKYSPHERE 2u /* SkySphere       material.rs:65-89 */
+#define MRT_BG_CUBEMAP 3u   /* CubeMap         material.rs:91-190 */
 typedef struct {
   uint32_t kind;
   uint32_t surface;
   float color[3];
+  /* CubeMap: x_pos, x_neg, y_pos, y_neg, z_pos, z_neg surfaces and the
+   * direction transform (column-major 4x4, CubeMap::new material.rs:102-118) */
+  uint32_t faces[6];
+  float transform[16];
 } mrt_background;
 
 /* Volume::new(Sphere::new((), center, radius), density, albedo): a constant-
@@ -311,6 +328,14 @@ int mrt_builder_add_volume(mrt_builder* b, const float* center, float radius, fl
 /* Mix::new(ratio, left, right): returns the material index */
 int mrt_builder_mix(mrt_builder* b, float ratio, uint32_t left, uint32_t right);
 int mrt_builder_background(mrt_builder* b, uint32_t kind, uint32_t surface, float r, float g, float bl);
+/* CubeMap::new(x_pos, x_neg, y_pos, y_neg, z_pos, z_neg, rotation) — faces are surface indices */
+int mrt_builder_background_cubemap(mrt_builder* b, const uint32_t* faces /*6*/, const float* rotation /*3*/);
+/* YCbCrTexture::load_png(luma, chroma, _): two texture surfaces -> a new surface index */
+int mrt_builder_ycbcr(mrt_builder* b, uint32_t luma, uint32_t chroma);
+/* TextureBlend::new(mode, left, right) -> a new surface index */
+int mrt_builder_blend(mrt_builder* b, uint32_t mode, uint32_t left, uint32_t right);
+/* SolidColorFallback::new(color, surface) -> a new surface index */
+int mrt_builder_fallback(mrt_builder* b, float r, float g, float bl, float a, uint32_t surface);
 /* world objects (World::add, world.rs:112-115) */
 int mrt_builder_add_sphere(mrt_builder* b, uint32_t material, float cx, float cy, float cz, float radius);
 int mrt_builder_add_triangle(mrt_builder* b, uint32_t material, const float* abc /*9*/);

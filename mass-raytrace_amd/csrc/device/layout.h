@@ -31,14 +31,37 @@ enum : uint32_t { KIND_BOX = 1, KIND_SPHERE = 2, KIND_TRI = 3, KIND_INST = 4, KI
 constexpr uint32_t KIND_END = 0;
 enum : uint32_t { TRI_FLAG_ALPHA = 1u, TRI_FLAG_UV = 2u };
 
+// Composite surfaces (YCbCrTexture, TextureBlend, SolidColorFallback,
+// texture.rs:197-357) run as small postfix programs over a V4 stack:
+//   SOLID    push color                TEXTURE  push get_f(tex)
+//   YCBCR    pop chroma, luma; push    BLEND    pop right, left; push blend(arg)
+//   FALLBACK pop c; push color*(1-c.w) + c*c.w
+// A YCbCr node is emitted as TEXTURE luma, TEXTURE chroma, YCBCR, so operands
+// are sampled in the reference's order (left before right, luma before chroma).
+constexpr uint32_t SURF_PROGRAM = 0xFFu;  // surf_kind of a composite surface reference
+constexpr uint32_t kSurfStack = 4;        // deepest operand stack a program may need
+struct GpuSurfOp {
+  uint32_t op, tex, arg, pad;
+  float color[4];
+};
+// A resolved surface: SOLID (color), TEXTURE (index = texture) or
+// SURF_PROGRAM (index = first op, len = op count).
+struct GpuSurfRef {
+  uint32_t kind, index, len, pad;
+  float color[4];
+};
+
 // Flattened material: surface resolved in place.
 //   q0 = {kind, surf_kind, texture, param bits}
 //   q1 = {color/emit rgba as float bits}
+//   q2 = {left, right, surf_len, 0}
 struct GpuMaterial {
   uint32_t kind, surf_kind, texture;
   float param;     // Metal fuzz, Dielectric/Specular refraction index, Mix ratio
   float color[4];  // SolidColor rgba (Lambertian/Metal/Specular), emit rgb (DiffuseLight), albedo (Isotrophic)
-  uint32_t left, right, pad0, pad1;  // Mix children
+  uint32_t left, right;  // Mix children
+  uint32_t surf_len;     // SURF_PROGRAM: op count (texture = first op)
+  uint32_t pad1;
 };
 
 struct GpuTexture {
@@ -74,10 +97,12 @@ struct DevScene {
   const uint32_t* vol_mat;  // Volume: its Isotrophic material
   const float* ln_table;    // ln(m * 2^-23) for every m < 2^23 (host libm logf), when volumes exist
   uint32_t n_vol;
+  const GpuSurfOp* surf_ops;
+  uint32_t n_surf_ops;
   uint32_t bg_kind;
-  uint32_t bg_texture;  // SkySphere texture (surface must be a texture or solid)
-  uint32_t bg_surf_kind;
   float bg_color[4];
+  const GpuSurfRef* bg_faces;  // SkySphere: 1 surface; CubeMap: x_pos x_neg y_pos y_neg z_pos z_neg
+  const float* bg_m;           // CubeMap transform, column-major 4x4
 };
 
 }  // namespace mrt

@@ -96,9 +96,57 @@ MRT_DEV V4 texture_get_f(const DevScene& S, uint32_t tex, V2 uv, LocalCounters& 
   return p1 * tt + p0 * (1.0f - tt);
 }
 
+// YCbCrTexture::get_f tail (texture.rs:233-249): YUV_TRANSFORM as a point
+// transform (generic.rs:105-115), clamp to [0,1], powf(2.2); alpha 1.
+MRT_DEV V4 ycbcr(V4 luma, V4 chroma) {
+  constexpr float KR = 0.2126f, KG = 0.7152f, KB = 0.0722f;
+  const M4 m{V4{1.0f, 1.0f, 1.0f, 0.0f}, V4{0.0f, -(KB / KG) * (2.0f - 2.0f * KB), 2.0f - 2.0f * KB, 0.0f},
+             V4{2.0f - 2.0f * KR, -(KR / KG) * (2.0f - 2.0f * KR), 0.0f, 0.0f}, V4{0.0f, 0.0f, 0.0f, 1.0f}};
+  V3 c = transform(m, V3{luma.x, chroma.x - 0.5f, chroma.y - 0.5f}, 1.0f);
+  c = V3{fmaxf(fminf(c.x, 1.0f), 0.0f), fmaxf(fminf(c.y, 1.0f), 0.0f), fmaxf(fminf(c.z, 1.0f), 0.0f)};
+  return V4{powf(c.x, 2.2f), powf(c.y, 2.2f), powf(c.z, 2.2f), 1.0f};
+}
+MRT_DEV V4 vmin4(V4 a, V4 b) { return V4{fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z), fminf(a.w, b.w)}; }
+MRT_DEV V4 vmax4(V4 a, V4 b) { return V4{fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w)}; }
+
+// A composite surface's postfix program (layout.h). The operand stack is
+// kSurfStack registers shifted on push/pop (static indices only, so it never
+// lives in scratch); only the EXT kernel variants contain this code.
+MRT_DEV V4 surface_program(const DevScene& S, uint32_t start, uint32_t len, V2 uv, LocalCounters& lc) {
+  static_assert(kSurfStack == 4, "stack shifts below are written for 4 slots");
+  V4 s0{}, s1{}, s2{}, s3{};
+  for (uint32_t i = 0; i < len; ++i) {
+    const GpuSurfOp o = S.surf_ops[MRT_IDX(S, start + i, S.n_surf_ops, 17)];
+    const V4 color{o.color[0], o.color[1], o.color[2], o.color[3]};
+    if (o.op == MRT_SURF_SOLID || o.op == MRT_SURF_TEXTURE) {  // push
+      const V4 v = o.op == MRT_SURF_TEXTURE ? texture_get_f(S, o.tex, uv, lc) : color;
+      s3 = s2, s2 = s1, s1 = s0, s0 = v;
+    } else if (o.op == MRT_SURF_FALLBACK) {  // SolidColorFallback::get_f (texture.rs:353-356)
+      s0 = (color * (1.0f - s0.w)) + (s0 * s0.w);
+    } else {  // binary: left = s1, right = s0
+      V4 v;
+      if (o.op == MRT_SURF_YCBCR) v = ycbcr(s1, s0);
+      else if (o.arg == MRT_BLEND_LIGHTEN) v = vmax4(s1, s0);  // BlendMode::blend (texture.rs:260-267)
+      else if (o.arg == MRT_BLEND_DARKEN) v = vmin4(s1, s0);
+      else if (o.arg == MRT_BLEND_ADDITION) v = vmin4(s1 + s0, V4{1.0f, 1.0f, 1.0f, 1.0f});
+      else v = vmax4(s1 - s0, V4{0.0f, 0.0f, 0.0f, 0.0f});
+      s0 = v, s1 = s2, s2 = s3;
+    }
+  }
+  return s0;
+}
+
+template <bool EXT>
+MRT_DEV V4 surface_ref_get_f(const DevScene& S, uint32_t kind, uint32_t index, uint32_t len, const float* color,
+                             V2 uv, LocalCounters& lc) {
+  if (kind == MRT_SURF_TEXTURE) return texture_get_f(S, index, uv, lc);
+  if (EXT && kind == SURF_PROGRAM) return surface_program(S, index, len, uv, lc);
+  return V4{color[0], color[1], color[2], color[3]};
+}
+
+template <bool EXT>
 MRT_DEV V4 surface_get_f(const DevScene& S, const GpuMaterial& m, V2 uv, LocalCounters& lc) {
-  if (m.surf_kind == MRT_SURF_TEXTURE) return texture_get_f(S, m.texture, uv, lc);
-  return V4{m.color[0], m.color[1], m.color[2], m.color[3]};
+  return surface_ref_get_f<EXT>(S, m.surf_kind, m.texture, m.surf_len, m.color, uv, lc);
 }
 
 // ---- primitive tests -------------------------------------------------------
@@ -249,7 +297,7 @@ MRT_DEV void tri_bary(const TriShade& s, V3 point, float& a0, float& a1, float& 
 
 // Material::alpha_test of the triangle's OWN material (geom.rs:567-571,
 // material.rs:222-224,281-283): surface alpha != 0.
-template <bool RNG>
+template <bool RNG, bool EXT>
 MRT_DEV bool tri_alpha_pass(const DevScene& S, uint32_t id, V3 o, V3 d, float t, PathRng& rng, LocalCounters& lc) {
   TriShade s = load_tri(S, id);
   V3 point = o + d * t;
@@ -262,7 +310,7 @@ MRT_DEV bool tri_alpha_pass(const DevScene& S, uint32_t id, V3 o, V3 d, float t,
     while (m.kind == MRT_MAT_MIX) m = S.materials[MRT_IDX(S, rng.f32() < m.param ? m.left : m.right, S.n_materials, 4)];
   // Lambertian/Metal alpha_test; Specular's forwards to its inner Lambertian
   if (m.kind != MRT_MAT_LAMBERTIAN && m.kind != MRT_MAT_METAL && m.kind != MRT_MAT_SPECULAR) return true;
-  return surface_get_f(S, m, uv, lc).w != 0.0f;
+  return surface_get_f<EXT>(S, m, uv, lc).w != 0.0f;
 }
 
 MRT_DEV void load_m12(const float* p, V3& c0, V3& c1, V3& c2, V3& c3) {
@@ -501,7 +549,8 @@ MRT_DEV bool volume_hit(const DevScene& S, const TravIn& in, Trav& t, uint4 s0, 
   return true;
 }
 
-template <bool COUNT, bool ALPHA, bool RNG = false>
+// ALPHA: 0 no alpha tests, 1 alpha tests, 2 alpha tests over EXT surfaces
+template <bool COUNT, uint32_t ALPHA, bool RNG = false>
 MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
   const DevScene& S = in.S;
   const uint4 s0 = t.s0, s1 = t.s1;
@@ -516,7 +565,7 @@ MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
     V3 a{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, ab{u2f(s0.w), u2f(s1.x), u2f(s1.y)}, ac{u2f(s2.x), u2f(s2.y), u2f(s2.z)};
     float th;
     if (tri_hit(a, ab, ac, t.r.o, t.r.d, in.tmin, t.best, th)) {
-      if (!ALPHA || !(s2.w & TRI_FLAG_ALPHA) || tri_alpha_pass<RNG>(S, s1.z, t.r.o, t.r.d, th, t.rng, lc)) {
+      if (!ALPHA || !(s2.w & TRI_FLAG_ALPHA) || tri_alpha_pass<RNG, ALPHA == 2>(S, s1.z, t.r.o, t.r.d, th, t.rng, lc)) {
         t.best = th;
         t.prim = make_ref(MRT_REF_TRIANGLE, s1.z);
         t.hit_ret = t.ret;
@@ -560,7 +609,7 @@ MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
 
 // Whole traversal of pool ray `ray` (one ray per thread); RNG: the
 // traversal's draws come from (and advance) `rng`.
-template <bool COUNT, bool RNG = false>
+template <bool COUNT, bool RNG = false, bool EXT = false>
 MRT_DEV Hit closest_hit(const TravIn& in, uint32_t ray, float tmax, LocalCounters& lc, PathRng& rng) {
   Trav t;
   trav_init(in, t, ray, tmax);
@@ -569,7 +618,7 @@ MRT_DEV Hit closest_hit(const TravIn& in, uint32_t ray, float tmax, LocalCounter
     if (trav_at_box(t))
       trav_box<COUNT>(in, t, lc);
     else
-      trav_prim<COUNT, true, RNG>(in, t, lc);
+      trav_prim<COUNT, EXT ? 2u : 1u, RNG>(in, t, lc);
   }
   if (RNG) rng = t.rng;
   return trav_hit(in, t);
@@ -690,6 +739,7 @@ MRT_DEV void camera_ray(const DevCamera& cam, uint32_t x, uint32_t y, uint32_t W
   camera_ray_uv(cam, u, v, rng, o, d);
 }
 
+template <bool EXT>
 MRT_DEV V3 background(const DevScene& S, V3 d, LocalCounters& lc) {
   if (S.bg_kind == MRT_BG_SOLID) return V3{S.bg_color[0], S.bg_color[1], S.bg_color[2]};
   if (S.bg_kind == MRT_BG_SKY) {
@@ -697,12 +747,37 @@ MRT_DEV V3 background(const DevScene& S, V3 d, LocalCounters& lc) {
     float t = 0.5f * (ud.y + 1.0f);
     return (fill3(1.0f) * (1.0f - t)) + (V3{0.5f, 0.7f, 1.0f} * t);
   }
-  V3 p = unit(d);
-  float theta = acosf(p.y);
-  float phi = atan2f(p.z * -1.0f, p.x) + kPi;
-  V2 uv{phi / (2.0f * kPi), theta / kPi};
-  V4 px = S.bg_surf_kind == MRT_SURF_TEXTURE ? texture_get_f(S, S.bg_texture, uv, lc)
-                                             : V4{S.bg_color[0], S.bg_color[1], S.bg_color[2], S.bg_color[3]};
+  V2 uv{0.0f, 0.0f};
+  uint32_t face = 0;
+  if (!EXT || S.bg_kind == MRT_BG_SKYSPHERE) {
+    V3 p = unit(d);
+    float theta = acosf(p.y);
+    float phi = atan2f(p.z * -1.0f, p.x) + kPi;
+    uv = V2{phi / (2.0f * kPi), theta / kPi};
+  } else if (EXT) {  // CubeMap::background (material.rs:122-189); y faces swapped as in the reference
+    const float* mf = S.bg_m;
+    const M4 m{V4{mf[0], mf[1], mf[2], mf[3]}, V4{mf[4], mf[5], mf[6], mf[7]}, V4{mf[8], mf[9], mf[10], mf[11]},
+               V4{mf[12], mf[13], mf[14], mf[15]}};
+    V3 p = transform(m, d, 0.0f);
+    V3 a{fabsf(p.x), fabsf(p.y), fabsf(p.z)};
+    float max_axis = 0.0f, u = 0.0f, v = 0.0f;
+    if (a.x >= a.y && a.x >= a.z) {
+      if (p.x > 0.0f) face = 0, u = p.z * -1.0f, v = p.y;
+      else face = 1, u = p.z, v = p.y;
+      max_axis = a.x;
+    } else if (a.y >= a.x && a.y >= a.z) {
+      if (p.y > 0.0f) face = 3, u = p.x, v = p.z * -1.0f;
+      else face = 2, u = p.x, v = p.z;
+      max_axis = a.y;
+    } else if (a.z >= a.x && a.z >= a.y) {
+      if (p.z > 0.0f) face = 4, u = p.x, v = p.y;
+      else face = 5, u = p.x * -1.0f, v = p.y;
+      max_axis = a.z;
+    }
+    uv = V2{0.5f * (u / max_axis + 1.0f), 0.5f * (v / max_axis + 1.0f)};
+  }
+  const GpuSurfRef f = S.bg_faces[face];
+  V4 px = surface_ref_get_f<EXT>(S, f.kind, f.index, f.len, f.color, uv, lc);
   return V3{px.x, px.y, px.z};
 }
 
@@ -719,16 +794,18 @@ MRT_DEV uint32_t mix_pick(const DevScene& S, uint32_t mi, PathRng& rng) {
 }
 
 // Lambertian::scatter (material.rs:203-215)
+template <bool EXT>
 MRT_DEV void lambertian(const DevScene& S, const GpuMaterial& m, const Surf& s, PathRng& rng, V3& atten, V3& new_d,
                         LocalCounters& lc) {
   V3 dir = s.normal + unit(random_in_unit_sphere(rng));
   if (near_zero(dir)) dir = s.normal;
-  V4 c = surface_get_f(S, m, s.has_uv ? s.uv : V2{0, 0}, lc);
+  V4 c = surface_get_f<EXT>(S, m, s.has_uv ? s.uv : V2{0, 0}, lc);
   atten = V3{c.x, c.y, c.z};
   new_d = dir;
 }
 
 // Hit::emit then Hit::scatter (world.rs:69-70), in that order of RNG draws.
+template <bool EXT>
 MRT_DEV bool scatter(const DevScene& S, const Surf& s, V3 d, PathRng& rng, V3& emitted, V3& atten, V3& new_d,
                      LocalCounters& lc) {
   emitted = V3{0, 0, 0};
@@ -740,13 +817,13 @@ MRT_DEV bool scatter(const DevScene& S, const Surf& s, V3 d, PathRng& rng, V3& e
   V2 uv = s.has_uv ? s.uv : V2{0, 0};
   switch (m.kind) {
     case MRT_MAT_LAMBERTIAN:
-      lambertian(S, m, s, rng, atten, new_d, lc);
+      lambertian<EXT>(S, m, s, rng, atten, new_d, lc);
       return true;
     case MRT_MAT_METAL: {
       V3 reflected = reflect(unit(d), s.normal);
       V3 dir = reflected + (random_in_unit_sphere(rng) * m.param);
       if (dot(dir, s.normal) > 0.0f) {
-        V4 c = surface_get_f(S, m, uv, lc);
+        V4 c = surface_get_f<EXT>(S, m, uv, lc);
         atten = V3{c.x, c.y, c.z};
         new_d = dir;
         return true;
@@ -763,7 +840,7 @@ MRT_DEV bool scatter(const DevScene& S, const Surf& s, V3 d, PathRng& rng, V3& e
       if (cannot_refract || reflectance(cos_theta, ratio) > rng.f32()) {
         new_d = reflect(ud, s.normal);
       } else if (m.kind == MRT_MAT_SPECULAR) {
-        lambertian(S, m, s, rng, atten, new_d, lc);  // return self.inner.scatter(ray, hit)
+        lambertian<EXT>(S, m, s, rng, atten, new_d, lc);  // return self.inner.scatter(ray, hit)
         return true;
       } else {
         new_d = refract(ud, s.normal, ratio);

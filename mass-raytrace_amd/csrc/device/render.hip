@@ -175,7 +175,7 @@ constexpr uint32_t kIdle = 0xFFFFFFFFu;  // Trav.ray of a lane without a ray
 // each ray carries its path stream through the traversal and stores it back.
 // (R > 1 would interleave R rays per lane — software ILP; measured slower at
 // its 84 VGPRs, so only R = 1 is instantiated.)
-template <bool COUNT, bool LDS, bool ALPHA, bool RNG>
+template <bool COUNT, bool LDS, uint32_t ALPHA, bool RNG>
 __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   DevCounters* cnt, float tmin, float tmax, TraceTune tune) {
   constexpr int R = 1;
@@ -304,15 +304,16 @@ __global__ __launch_bounds__(kBlock) void k_trace_simple(DevScene S, PathBufs in
 // ray (o, d): adds T * emitted (hit) or T * background (miss) to L; on a
 // scatter that continues (and depth left) moves (o, d) to the scattered ray,
 // multiplies T by the attenuation and returns true.
+template <bool EXT>
 MRT_DEV bool shade_step(const DevScene& S, uint32_t max_depth, const Hit& h, V3& o, V3& d, V3& T, V3& L, uint32_t& k,
                         PathRng& rng, LocalCounters& lc, uint32_t& nbounce) {
   if (h.prim == kRefNone) {
-    L = L + T * background(S, d, lc);
+    L = L + T * background<EXT>(S, d, lc);
     return false;
   }
   Surf s = resolve_hit(S, o, d, h);
   V3 emitted, atten, nd;
-  bool cont = scatter(S, s, d, rng, emitted, atten, nd, lc);
+  bool cont = scatter<EXT>(S, s, d, rng, emitted, atten, nd, lc);
   L = L + T * emitted;
   if (!cont) return false;
   T = T * atten;
@@ -323,7 +324,7 @@ MRT_DEV bool shade_step(const DevScene& S, uint32_t max_depth, const Hit& h, V3&
   return k < max_depth;  // trace(depth 0) returns (0, 0)
 }
 
-template <bool COUNT>
+template <bool COUNT, bool EXT>
 __global__ __launch_bounds__(kBlock, 8) void k_shade(DevScene S, DevCamera cam, RenderParams rp, PathBufs in,
                                                   PathBufs out, const uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   uint32_t* work, float4* results, DevCounters* cnt) {
@@ -349,7 +350,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_shade(DevScene S, DevCamera cam, 
     uint32_t g = __float_as_uint(ro.w), k = __float_as_uint(rd.w);
     PathRng rng{(unsigned long long)rs.x | ((unsigned long long)rs.y << 32),
                 (unsigned long long)rs.z | ((unsigned long long)rs.w << 32)};
-    const bool cont = shade_step(S, rp.max_depth, h, o, d, T, L, k, rng, lc, nbounce);
+    const bool cont = shade_step<EXT>(S, rp.max_depth, h, o, d, T, L, k, rng, lc, nbounce);
     if (cont) {
       alive = true;
       ro = make_float4(o.x, o.y, o.z, __uint_as_float(g));
@@ -468,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void k_render(DevScene S, DevCamera cam, Re
         nh += h.prim != kRefNone;
         const float4 o4 = slot_ro[slot], d4 = slot_rd[slot];
         V3 o{o4.x, o4.y, o4.z}, d{d4.x, d4.y, d4.z};
-        if (shade_step(S, rp.max_depth, h, o, d, T, L, k, rng, lc, nbounces)) {
+        if (shade_step<false>(S, rp.max_depth, h, o, d, T, L, k, rng, lc, nbounces)) {
           slot_ro[slot] = make_float4(o.x, o.y, o.z, 0.0f);
           slot_rd[slot] = make_float4(d.x, d.y, d.z, 0.0f);
           trav_init(tin, t, slot, INFINITY);
@@ -627,7 +628,7 @@ __global__ __launch_bounds__(kBlock) void k_max_u32(const uint32_t* v, uint32_t 
 
 // Camera::albedo_normal for pixel p (one ray, no jitter). The rays go through
 // ray_ro/ray_rd so that the traversal can re-read them (TravIn).
-template <bool RNG>
+template <bool RNG, bool EXT>
 __global__ __launch_bounds__(kBlock) void k_prepass(DevScene S, DevCamera cam, uint32_t W, uint32_t H,
                                                     unsigned long long seed, float4* ray_ro, float4* ray_rd,
                                                     float* albedo, float* normal) {
@@ -641,15 +642,15 @@ __global__ __launch_bounds__(kBlock) void k_prepass(DevScene S, DevCamera cam, u
   ray_rd[p] = make_float4(d.x, d.y, d.z, 0.0f);
   const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), ray_ro, ray_rd, kTmin};
   LocalCounters lc;
-  const Hit h = closest_hit<false, RNG>(tin, p, INFINITY, lc, rng);
+  const Hit h = closest_hit<false, RNG, EXT>(tin, p, INFINITY, lc, rng);
   V3 a{0.0f, 0.0f, 0.0f}, n{0.0f, 0.0f, 0.0f};
   if (h.prim != kRefNone) {
     Surf s = resolve_hit(S, o, d, h);
     V3 emitted, atten, nd;
-    a = scatter(S, s, d, rng, emitted, atten, nd, lc) ? atten : emitted;
+    a = scatter<EXT>(S, s, d, rng, emitted, atten, nd, lc) ? atten : emitted;
     n = s.normal;
   } else {
-    a = background(S, d, lc);
+    a = background<EXT>(S, d, lc);
   }
   albedo[3 * (size_t)p] = a.x, albedo[3 * (size_t)p + 1] = a.y, albedo[3 * (size_t)p + 2] = a.z;
   normal[3 * (size_t)p] = n.x, normal[3 * (size_t)p + 1] = n.y, normal[3 * (size_t)p + 2] = n.z;
@@ -809,6 +810,7 @@ struct mrt_ctx {
   std::map<std::pair<const void*, size_t>, uint32_t> grids;  // persistent grid per (kernel, LDS bytes)
   bool scene_alpha = true;  // the scene has alpha-tested triangles
   bool scene_rng = false;   // the traversal draws random numbers (Volume, Mix alpha tests)
+  bool scene_ext = false;   // composite surfaces or a CubeMap background (the EXT kernel variants)
   TraceTune tune;
   // k_render: per-lane current world ray; event pair timing one launch
   float4* slot_ro = nullptr;
@@ -899,7 +901,7 @@ uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem) {
   return g;
 }
 
-template <bool LDS, bool ALPHA, bool RNG>
+template <bool LDS, uint32_t ALPHA, bool RNG>
 void launch_trace_r(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
                     float tmin, float tmax) {
   const size_t smem = LDS ? (size_t)c->S.n_slots * 16 : 0;
@@ -913,7 +915,7 @@ void launch_trace_r(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& 
                        q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
 }
 
-template <bool LDS, bool ALPHA>
+template <bool LDS, uint32_t ALPHA>
 void launch_trace_v(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
                     float tmin, float tmax) {
   if (c->scene_rng)
@@ -924,16 +926,22 @@ void launch_trace_v(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& 
 
 void launch_trace(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
                   float tmin, float tmax) {
+  // alpha tests: none / plain surfaces / composite surfaces (EXT)
+  const uint32_t alpha = c->scene_alpha ? (c->scene_ext ? 2u : 1u) : 0u;
   if (c->trace_lds) {
-    if (c->scene_alpha)
-      launch_trace_v<true, true>(c, st, q, in, cur, count, tmin, tmax);
+    if (alpha == 2)
+      launch_trace_v<true, 2>(c, st, q, in, cur, count, tmin, tmax);
+    else if (alpha == 1)
+      launch_trace_v<true, 1>(c, st, q, in, cur, count, tmin, tmax);
     else
-      launch_trace_v<true, false>(c, st, q, in, cur, count, tmin, tmax);
+      launch_trace_v<true, 0>(c, st, q, in, cur, count, tmin, tmax);
   } else {
-    if (c->scene_alpha)
-      launch_trace_v<false, true>(c, st, q, in, cur, count, tmin, tmax);
+    if (alpha == 2)
+      launch_trace_v<false, 2>(c, st, q, in, cur, count, tmin, tmax);
+    else if (alpha == 1)
+      launch_trace_v<false, 1>(c, st, q, in, cur, count, tmin, tmax);
     else
-      launch_trace_v<false, false>(c, st, q, in, cur, count, tmin, tmax);
+      launch_trace_v<false, 0>(c, st, q, in, cur, count, tmin, tmax);
   }
   HIP_CHECK(hipGetLastError());
 }
@@ -1093,9 +1101,13 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
   const bool count = (a->flags & MRT_RENDER_COUNTERS) != 0;
   // results slab <= kResultsMax samples (16 B each); pool <= c->pool_paths
   uint32_t spp_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(a->spp_count, kResultsMax / n_pix));
+  if ((a->flags & MRT_RENDER_SIMPLE_TRACE) && c->scene_ext)
+    throw ApiError{MRT_ERR_INVALID, "MRT_RENDER_SIMPLE_TRACE does not support composite surfaces or CubeMap backgrounds"};
   if ((a->flags & MRT_RENDER_FUSED) && !(a->flags & MRT_RENDER_SIMPLE_TRACE)) {
     if (c->scene_rng)
       throw ApiError{MRT_ERR_INVALID, "MRT_RENDER_FUSED does not support scenes whose traversal draws (Volume, Mix alpha)"};
+    if (c->scene_ext)
+      throw ApiError{MRT_ERR_INVALID, "MRT_RENDER_FUSED does not support composite surfaces or CubeMap backgrounds"};
     render_fused(c, a, pl.first, n_pix, spp_chunk, d_rgb, d_b, st);
     return;
   }
@@ -1181,12 +1193,12 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
             m[1] = next_event();
             HIP_CHECK(hipEventRecord(m[1], q.stream));
           }
-          if (count)
-            hipLaunchKernelGGL(k_shade<true>, dim3(grid), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, q.bufs[cur],
+          {
+            auto* shade = count ? (c->scene_ext ? k_shade<true, true> : k_shade<true, false>)
+                                : (c->scene_ext ? k_shade<false, true> : k_shade<false, false>);
+            hipLaunchKernelGGL(shade, dim3(grid), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, q.bufs[cur],
                                q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, c->work, c->results, c->d_cnt);
-          else
-            hipLaunchKernelGGL(k_shade<false>, dim3(grid), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, q.bufs[cur],
-                               q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, c->work, c->results, c->d_cnt);
+          }
           HIP_CHECK(hipGetLastError());
           if (timing) {
             m[2] = next_event();
@@ -1358,6 +1370,9 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
            o_vnid = sec(hs.vol_nid.size() * 4), o_vmat = sec(hs.vol_mat.size() * 4);
     const std::vector<float>& ln_table = hs.ln_table;
     const size_t o_ln = sec(ln_table.size() * 4);
+    const size_t o_sops = sec(hs.surf_ops.size() * sizeof(GpuSurfOp));
+    const size_t o_bgf = sec(hs.bg_faces.size() * sizeof(GpuSurfRef));
+    const size_t o_bgm = sec(sizeof(hs.bg_m));
     if (c->scene_mem) HIP_CHECK(hipFree(c->scene_mem));
     c->scene_mem = nullptr;
     c->has_scene = false;
@@ -1380,6 +1395,9 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     up(o_mat, hs.materials.data(), hs.materials.size() * sizeof(GpuMaterial));
     up(o_tex, hs.textures.data(), hs.textures.size() * sizeof(GpuTexture));
     up(o_texel, hs.texels.data(), hs.texels.size() * 4);
+    up(o_sops, hs.surf_ops.data(), hs.surf_ops.size() * sizeof(GpuSurfOp));
+    up(o_bgf, hs.bg_faces.data(), hs.bg_faces.size() * sizeof(GpuSurfRef));
+    up(o_bgm, hs.bg_m, sizeof(hs.bg_m));
     DevScene S{};
     S.slots = (const uint32_t*)(base + o_slots);
     S.world_begin = hs.world_begin;
@@ -1409,9 +1427,11 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     S.n_texels = (uint32_t)hs.texels.size();
     S.dbg = c->dbg;
     S.bg_kind = hs.bg_kind;
-    S.bg_texture = hs.bg_texture;
-    S.bg_surf_kind = hs.bg_surf_kind;
     for (int k = 0; k < 4; ++k) S.bg_color[k] = hs.bg_color[k];
+    S.surf_ops = (const GpuSurfOp*)(base + o_sops);
+    S.n_surf_ops = (uint32_t)hs.surf_ops.size();
+    S.bg_faces = (const GpuSurfRef*)(base + o_bgf);
+    S.bg_m = (const float*)(base + o_bgm);
     c->S = S;
     c->scene_bytes = off;
     const size_t lds_bytes = (size_t)S.n_slots * 16;
@@ -1419,6 +1439,7 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     c->trace_lds = lds_bytes <= kTraceLdsMaxBytes && !(no_lds && no_lds[0] == '0');
     c->scene_alpha = hs.has_alpha;
     c->scene_rng = hs.trav_rng;
+    c->scene_ext = !hs.surf_ops.empty() || hs.bg_kind == MRT_BG_CUBEMAP;
     c->has_scene = true;
   });
 }
@@ -1627,12 +1648,10 @@ int mrt_prepass_device(mrt_ctx* c, uint32_t W, uint32_t H, uint64_t seed, float*
     wait_queues(c, st);
     const uint32_t n = W * H;
     ensure_slots(c, n);  // the pre-pass rays
-    if (c->scene_rng)
-      hipLaunchKernelGGL(k_prepass<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c->S, c->cam, W, H,
-                         (unsigned long long)seed, c->slot_ro, c->slot_rd, d_albedo, d_normal);
-    else
-      hipLaunchKernelGGL(k_prepass<false>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c->S, c->cam, W, H,
-                         (unsigned long long)seed, c->slot_ro, c->slot_rd, d_albedo, d_normal);
+    auto* prepass = c->scene_rng ? (c->scene_ext ? k_prepass<true, true> : k_prepass<true, false>)
+                                 : (c->scene_ext ? k_prepass<false, true> : k_prepass<false, false>);
+    hipLaunchKernelGGL(prepass, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c->S, c->cam, W, H,
+                       (unsigned long long)seed, c->slot_ro, c->slot_rd, d_albedo, d_normal);
     HIP_CHECK(hipGetLastError());
   });
 }

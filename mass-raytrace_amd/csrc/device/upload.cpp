@@ -16,6 +16,125 @@ uint32_t fbits(float f) {
   return u;
 }
 
+// Surfaces -> GpuSurfRef; composites become postfix programs (layout.h).
+struct SurfResolver {
+  const mrt_scene_desc& d;
+  HostScene& s;
+  std::string& err;
+  std::unordered_map<uint32_t, GpuSurfRef> memo;
+  std::vector<int8_t> tex_zero_alpha;  // per texture: some texel has alpha 0 (-1 = not yet scanned)
+  static constexpr uint32_t kMaxOps = 256;
+
+  bool fail(const char* m) {
+    err = m;
+    return false;
+  }
+  // Appends surface i's program; `depth` = operand stack slots it needs.
+  bool emit(uint32_t i, uint32_t& depth) {
+    const mrt_surface& sf = d.surfaces[i];
+    GpuSurfOp op{};
+    op.op = sf.kind;
+    for (int k = 0; k < 4; ++k) op.color[k] = sf.color[k];
+    switch (sf.kind) {
+      case MRT_SURF_SOLID:
+        depth = 1;
+        break;
+      case MRT_SURF_TEXTURE:
+        if (sf.texture >= d.n_textures) return fail("surface texture out of range");
+        op.tex = sf.texture;
+        depth = 1;
+        break;
+      case MRT_SURF_YCBCR: {
+        if (sf.texture >= d.n_textures || sf.a >= d.n_textures) return fail("YCbCr texture out of range");
+        GpuSurfOp t{};
+        t.op = MRT_SURF_TEXTURE;
+        t.tex = sf.texture;
+        s.surf_ops.push_back(t);
+        t.tex = sf.a;
+        s.surf_ops.push_back(t);
+        depth = 2;
+        break;
+      }
+      case MRT_SURF_BLEND: {
+        if (sf.a >= i || sf.b >= i) return fail("blend operands must precede the blend in the surface table");
+        if (sf.mode > MRT_BLEND_SUBTRACTION) return fail("bad blend mode");
+        uint32_t dl, dr;
+        if (!emit(sf.a, dl) || !emit(sf.b, dr)) return false;
+        op.arg = sf.mode;
+        depth = dl > dr + 1 ? dl : dr + 1;
+        break;
+      }
+      case MRT_SURF_FALLBACK:
+        if (sf.a >= i) return fail("fallback surface must precede it in the surface table");
+        if (!emit(sf.a, depth)) return false;
+        break;
+      default:
+        return fail("bad surface kind");
+    }
+    s.surf_ops.push_back(op);
+    return true;
+  }
+  bool resolve(uint32_t i, GpuSurfRef& out) {
+    if (i >= d.n_surfaces) return fail("surface index out of range");
+    auto it = memo.find(i);
+    if (it != memo.end()) return (out = it->second, true);
+    const mrt_surface& sf = d.surfaces[i];
+    GpuSurfRef r{};
+    for (int k = 0; k < 4; ++k) r.color[k] = sf.color[k];
+    if (sf.kind == MRT_SURF_SOLID || sf.kind == MRT_SURF_TEXTURE) {
+      r.kind = sf.kind;
+      r.index = sf.kind == MRT_SURF_TEXTURE ? sf.texture : 0;
+      if (sf.kind == MRT_SURF_TEXTURE && sf.texture >= d.n_textures) return fail("surface texture out of range");
+    } else {
+      uint32_t start = (uint32_t)s.surf_ops.size(), depth = 0;
+      if (!emit(i, depth)) return false;
+      if (depth > kSurfStack) return fail("composite surface nested too deeply (operand stack > 4)");
+      if (s.surf_ops.size() - start > kMaxOps) return fail("composite surface program too long");
+      r.kind = SURF_PROGRAM;
+      r.index = start;
+      r.len = (uint32_t)s.surf_ops.size() - start;
+    }
+    memo[i] = r;
+    out = r;
+    return true;
+  }
+  bool texture_has_zero_alpha(uint32_t t) {
+    if (t >= d.n_textures) return false;
+    if (tex_zero_alpha.empty()) tex_zero_alpha.assign(d.n_textures, -1);
+    int8_t& z = tex_zero_alpha[t];
+    if (z < 0) {
+      const mrt_texture& tx = d.textures[t];
+      z = 0;
+      for (size_t k = 0; k < (size_t)tx.width * tx.height; ++k)
+        if (tx.rgba[4 * k + 3] == 0) {
+          z = 1;
+          break;
+        }
+    }
+    return z == 1;
+  }
+  // Can get_f(uv).w be 0 somewhere? (conservative: true means "run the alpha test")
+  bool may_zero_alpha(uint32_t i) {
+    if (i >= d.n_surfaces) return false;
+    const mrt_surface& sf = d.surfaces[i];
+    switch (sf.kind) {
+      case MRT_SURF_SOLID:
+        return sf.color[3] == 0.0f;
+      case MRT_SURF_TEXTURE:
+        return texture_has_zero_alpha(sf.texture);
+      case MRT_SURF_YCBCR:
+        return false;  // alpha is 1 (texture.rs:247)
+      case MRT_SURF_BLEND:
+        if (sf.a >= i || sf.b >= i) return false;
+        if (sf.mode == MRT_BLEND_DARKEN) return may_zero_alpha(sf.a) || may_zero_alpha(sf.b);
+        if (sf.mode == MRT_BLEND_SUBTRACTION) return true;
+        return may_zero_alpha(sf.a) && may_zero_alpha(sf.b);  // max / min(l+r, 1) of non-negative alphas
+      default:
+        return true;
+    }
+  }
+};
+
 struct Emitter {
   const mrt_scene_desc& d;
   HostScene& s;
@@ -92,8 +211,8 @@ struct Emitter {
   }
 
   // Triangle::intersect runs alpha_test only with uvs; it can reject only if
-  // the triangle's own material samples a texture holding a zero alpha.
-  std::vector<int8_t> tex_zero_alpha;  // per texture, computed once
+  // the triangle's own material's surface can have a zero alpha.
+  SurfResolver* surfaces = nullptr;
   bool mix_alpha = false;              // a uv triangle's alpha test draws random numbers
   bool needs_alpha(const mrt_triangle& t) {
     if (!(t.flags & MRT_TRI_HAS_UV) || t.material >= d.n_materials) return false;
@@ -103,22 +222,7 @@ struct Emitter {
       return true;
     }
     if (m.kind != MRT_MAT_LAMBERTIAN && m.kind != MRT_MAT_METAL && m.kind != MRT_MAT_SPECULAR) return false;
-    if (m.surface >= d.n_surfaces) return false;
-    const mrt_surface& sf = d.surfaces[m.surface];
-    if (sf.kind == MRT_SURF_SOLID) return sf.color[3] == 0.0f;
-    if (sf.texture >= d.n_textures) return false;
-    if (tex_zero_alpha.empty()) tex_zero_alpha.assign(d.n_textures, -1);
-    int8_t& z = tex_zero_alpha[sf.texture];
-    if (z < 0) {
-      const mrt_texture& tx = d.textures[sf.texture];
-      z = 0;
-      for (size_t i = 0; i < (size_t)tx.width * tx.height; ++i)
-        if (tx.rgba[4 * i + 3] == 0) {
-          z = 1;
-          break;
-        }
-    }
-    return z == 1;
+    return surfaces->may_zero_alpha(m.surface);
   }
 
   bool fail(const char* m) {
@@ -180,7 +284,8 @@ void put_m4_12(std::vector<float>& dst, const float* m16) {
 
 bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
   s = HostScene{};
-  Emitter e{d, s, err, {}, {}};
+  SurfResolver surf{d, s, err, {}, {}};
+  Emitter e{d, s, err, {}, &surf};
   // materials
   for (uint32_t i = 0; i < d.n_materials; ++i) {
     const mrt_material& m = d.materials[i];
@@ -190,11 +295,12 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
     if (m.kind > MRT_MAT_MIX) return (err = "bad material kind", false);
     if (m.kind == MRT_MAT_LAMBERTIAN || m.kind == MRT_MAT_METAL || m.kind == MRT_MAT_SPECULAR) {
       if (m.surface >= d.n_surfaces) return (err = "material surface out of range", false);
-      const mrt_surface& sf = d.surfaces[m.surface];
-      g.surf_kind = sf.kind;
-      g.texture = sf.texture;
-      if (sf.kind == MRT_SURF_TEXTURE && sf.texture >= d.n_textures) return (err = "surface texture out of range", false);
-      for (int k = 0; k < 4; ++k) g.color[k] = sf.color[k];
+      GpuSurfRef r;
+      if (!surf.resolve(m.surface, r)) return false;
+      g.surf_kind = r.kind;
+      g.texture = r.index;
+      g.surf_len = r.len;
+      for (int k = 0; k < 4; ++k) g.color[k] = r.color[k];
     } else if (m.kind == MRT_MAT_DIFFUSE_LIGHT || m.kind == MRT_MAT_ISOTROPHIC) {
       for (int k = 0; k < 3; ++k) g.color[k] = m.emit[k];  // emission / albedo
     } else if (m.kind == MRT_MAT_MIX) {
@@ -269,14 +375,15 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
   // background
   s.bg_kind = d.background.kind;
   for (int k = 0; k < 3; ++k) s.bg_color[k] = d.background.color[k];
-  if (d.background.kind == MRT_BG_SKYSPHERE) {
-    if (d.background.surface >= d.n_surfaces) return (err = "background surface out of range", false);
-    const mrt_surface& sf = d.background.surface < d.n_surfaces ? d.surfaces[d.background.surface] : mrt_surface{};
-    s.bg_surf_kind = sf.kind;
-    s.bg_texture = sf.texture;
-    if (sf.kind == MRT_SURF_TEXTURE && sf.texture >= d.n_textures) return (err = "background texture out of range", false);
-    for (int k = 0; k < 4; ++k) s.bg_color[k] = sf.color[k];
-  } else if (d.background.kind > MRT_BG_SKYSPHERE) {
+  if (d.background.kind == MRT_BG_SKYSPHERE || d.background.kind == MRT_BG_CUBEMAP) {
+    const bool cube = d.background.kind == MRT_BG_CUBEMAP;
+    for (int k = 0; k < (cube ? 6 : 1); ++k) {
+      GpuSurfRef r;
+      if (!surf.resolve(cube ? d.background.faces[k] : d.background.surface, r)) return false;
+      s.bg_faces.push_back(r);
+    }
+    if (cube) memcpy(s.bg_m, d.background.transform, sizeof(s.bg_m));
+  } else if (d.background.kind > MRT_BG_CUBEMAP) {
     return (err = "bad background kind", false);
   }
   // world region: World::objects in order

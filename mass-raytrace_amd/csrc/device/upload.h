@@ -29,8 +29,11 @@ struct HostScene {
   // instead of computing it, so the distance is the reference's to the bit
   // (32 MiB, built only when the scene has volumes).
   std::vector<float> ln_table;
-  uint32_t bg_kind = 0, bg_texture = 0, bg_surf_kind = 0;
+  std::vector<GpuSurfOp> surf_ops;
+  uint32_t bg_kind = 0;
   float bg_color[4] = {0, 0, 0, 0};
+  std::vector<GpuSurfRef> bg_faces;  // SkySphere 1, CubeMap 6
+  float bg_m[16] = {0};
   // statistics
   uint32_t n_box_records = 0, n_prim_records = 0, max_depth = 0;
 };

@@ -146,6 +146,46 @@ int mrt_builder_mix(mrt_builder* b, float ratio, uint32_t left, uint32_t right) 
   });
 }
 
+static const Surface& surf_at(mrt_builder* b, uint32_t i) {
+  if (i >= b->surfaces.size()) throw Error(MRT_ERR_INVALID, "surface index out of range");
+  return b->surfaces[i];
+}
+
+int mrt_builder_ycbcr(mrt_builder* b, uint32_t luma, uint32_t chroma) {
+  return guard(b, [&] {
+    const Surface &l = surf_at(b, luma), &c = surf_at(b, chroma);
+    if (l.kind != MRT_SURF_TEXTURE || c.kind != MRT_SURF_TEXTURE)
+      throw Error(MRT_ERR_INVALID, "YCbCr planes must be texture surfaces");
+    b->surfaces.push_back(YCbCrTexture(l.texture, c.texture));
+    return (int)b->surfaces.size() - 1;
+  });
+}
+
+int mrt_builder_blend(mrt_builder* b, uint32_t mode, uint32_t left, uint32_t right) {
+  return guard(b, [&] {
+    if (mode > MRT_BLEND_SUBTRACTION) throw Error(MRT_ERR_INVALID, "bad blend mode");
+    b->surfaces.push_back(TextureBlend(mode, surf_at(b, left), surf_at(b, right)));
+    return (int)b->surfaces.size() - 1;
+  });
+}
+
+int mrt_builder_fallback(mrt_builder* b, float r, float g, float bl, float a, uint32_t surface) {
+  return guard(b, [&] {
+    b->surfaces.push_back(SolidColorFallback(V4{r, g, bl, a}, surf_at(b, surface)));
+    return (int)b->surfaces.size() - 1;
+  });
+}
+
+int mrt_builder_background_cubemap(mrt_builder* b, const uint32_t* faces, const float* rotation) {
+  return guard(b, [&] {
+    if (!faces || !rotation) throw Error(MRT_ERR_INVALID, "null argument");
+    Surface f[6];
+    for (int k = 0; k < 6; ++k) f[k] = surf_at(b, faces[k]);
+    b->world->set_background(CubeMap(f, V3{rotation[0], rotation[1], rotation[2]}));
+    return 0;
+  });
+}
+
 static const Material& mat_at(mrt_builder* b, uint32_t i) {
   if (i >= b->materials.size()) throw Error(MRT_ERR_INVALID, "material index out of range");
   return b->materials[i];

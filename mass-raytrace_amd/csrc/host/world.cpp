@@ -149,7 +149,23 @@ uint32_t World::intern_texture(const SharedTexture& t) {
 uint32_t World::intern_surface(const Surface& s) {
   mrt_surface d{};
   d.kind = s.kind;
-  d.texture = s.kind == MRT_SURF_TEXTURE ? intern_texture(s.texture) : 0;
+  switch (s.kind) {  // operands first: their indices are lower than this one's
+    case MRT_SURF_TEXTURE:
+      d.texture = intern_texture(s.texture);
+      break;
+    case MRT_SURF_YCBCR:
+      d.texture = intern_texture(s.texture);
+      d.a = intern_texture(s.chroma);
+      break;
+    case MRT_SURF_BLEND:
+      d.mode = s.mode;
+      d.a = intern_surface(*s.left);
+      d.b = intern_surface(*s.right);
+      break;
+    case MRT_SURF_FALLBACK:
+      d.a = intern_surface(*s.left);
+      break;
+  }
   d.color[0] = s.color.x;
   d.color[1] = s.color.y;
   d.color[2] = s.color.z;
@@ -340,6 +356,15 @@ const mrt_scene_desc& World::desc() {
   bg.kind = background_.kind;
   put3(bg.color, background_.color);
   bg.surface = background_.kind == MRT_BG_SKYSPHERE ? intern_surface(background_.surface) : 0;
+  if (background_.kind == MRT_BG_CUBEMAP) {
+    for (int k = 0; k < 6; ++k) bg.faces[k] = intern_surface(background_.faces[k]);
+    const M4& m = background_.transform;
+    const V4 cols[4] = {m.c0, m.c1, m.c2, m.c3};
+    for (int c = 0; c < 4; ++c) {
+      bg.transform[4 * c + 0] = cols[c].x, bg.transform[4 * c + 1] = cols[c].y;
+      bg.transform[4 * c + 2] = cols[c].z, bg.transform[4 * c + 3] = cols[c].w;
+    }
+  }
   desc_.nodes = nodes_.data();
   desc_.n_nodes = (uint32_t)nodes_.size();
   desc_.roots = roots_.data();

@@ -61,10 +61,14 @@ struct Texture {  // texture.rs:21-27 (RGBA8 kept; decoded c/255.0 on use)
 };
 using SharedTexture = std::shared_ptr<Texture>;
 
-struct Surface {  // SolidColor(V4) or a shared Texture
+// SolidColor(V4), a shared Texture, or a composite over them (texture.rs:197-357)
+struct Surface {
   uint32_t kind = MRT_SURF_SOLID;
-  V4 color{1, 1, 1, 1};
-  SharedTexture texture;
+  V4 color{1, 1, 1, 1};    // SolidColor / SolidColorFallback colour
+  SharedTexture texture;   // Texture, YCbCr luma
+  SharedTexture chroma;    // YCbCr chroma
+  uint32_t mode = 0;       // TextureBlend mode
+  std::shared_ptr<const Surface> left, right;  // TextureBlend operands; Fallback's surface in `left`
 };
 inline Surface SolidColor(V4 c) {
   Surface s;
@@ -76,6 +80,29 @@ inline Surface TextureSurface(SharedTexture t) {
   Surface s;
   s.kind = MRT_SURF_TEXTURE;
   s.texture = std::move(t);
+  return s;
+}
+
+inline Surface YCbCrTexture(SharedTexture luma, SharedTexture chroma) {  // texture.rs:212-223
+  Surface s;
+  s.kind = MRT_SURF_YCBCR;
+  s.texture = std::move(luma);
+  s.chroma = std::move(chroma);
+  return s;
+}
+inline Surface TextureBlend(uint32_t mode, Surface l, Surface r) {  // texture.rs:309-317
+  Surface s;
+  s.kind = MRT_SURF_BLEND;
+  s.mode = mode;
+  s.left = std::make_shared<const Surface>(std::move(l));
+  s.right = std::make_shared<const Surface>(std::move(r));
+  return s;
+}
+inline Surface SolidColorFallback(V4 color, Surface inner) {  // texture.rs:341-345
+  Surface s;
+  s.kind = MRT_SURF_FALLBACK;
+  s.color = color;
+  s.left = std::make_shared<const Surface>(std::move(inner));
   return s;
 }
 
@@ -139,6 +166,8 @@ struct Background {
   uint32_t kind = MRT_BG_SOLID;
   V3 color{0, 0, 0};
   Surface surface;
+  Surface faces[6];  // CubeMap x_pos, x_neg, y_pos, y_neg, z_pos, z_neg
+  M4 transform{};    // CubeMap direction transform
 };
 inline Background SolidBackground(V3 c) {
   Background b;
@@ -155,6 +184,17 @@ inline Background SkySphere(Surface s) {
   Background b;
   b.kind = MRT_BG_SKYSPHERE;
   b.surface = std::move(s);
+  return b;
+}
+
+// CubeMap::new (material.rs:102-118): note the reference builds all three
+// factors with rotate_x.
+inline Background CubeMap(const Surface faces[6], V3 rotation) {
+  Background b;
+  b.kind = MRT_BG_CUBEMAP;
+  for (int k = 0; k < 6; ++k) b.faces[k] = faces[k];
+  b.transform = mrt::m4_mul(mrt::m4_mul(mrt::m4_rotate_x(rotation.x), mrt::m4_rotate_x(rotation.y)),
+                            mrt::m4_rotate_x(rotation.z));
   return b;
 }
 

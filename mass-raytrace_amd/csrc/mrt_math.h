@@ -54,6 +54,7 @@ MRT_HD V2 operator-(V2 a, V2 b) { return V2{a.x - b.x, a.y - b.y}; }
 MRT_HD V2 operator*(V2 a, float s) { return V2{a.x * s, a.y * s}; }
 
 MRT_HD V4 operator+(V4 a, V4 b) { return V4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
+MRT_HD V4 operator-(V4 a, V4 b) { return V4{a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w}; }
 MRT_HD V4 operator*(V4 a, float s) { return V4{a.x * s, a.y * s, a.z * s, a.w * s}; }
 
 MRT_HD float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }

@@ -26,11 +26,13 @@ LIB_PATH = (Path(_SEL) if _SEL.endswith(".so") else
 REPO = _HERE.parent.parent
 
 # ---- constants (massrt.h) --------------------------------------------------
-ABI_VERSION = 2  # MRT_ABI_VERSION this binding was written for
+ABI_VERSION = 3  # MRT_ABI_VERSION this binding was written for
 REF_NONE, REF_NODE, REF_SPHERE, REF_TRIANGLE, REF_INSTANCE, REF_MODEL, REF_VOLUME = range(7)
 MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_SPECULAR, MAT_ISOTROPHIC, MAT_MIX = range(8)
 WRAP_MIRROR, WRAP_REPEAT, WRAP_CLAMP = range(3)
-BG_SOLID, BG_SKY, BG_SKYSPHERE = range(3)
+BG_SOLID, BG_SKY, BG_SKYSPHERE, BG_CUBEMAP = range(4)
+SURF_SOLID, SURF_TEXTURE, SURF_YCBCR, SURF_BLEND, SURF_FALLBACK = range(5)
+BLEND_LIGHTEN, BLEND_DARKEN, BLEND_ADDITION, BLEND_SUBTRACTION = range(4)
 NO_MATERIAL = 0xFFFFFFFF
 RENDER_COUNTERS = 1
 RENDER_TIME_KERNELS = 2
@@ -80,7 +82,8 @@ class MrtMaterial(C.Structure):
 
 
 class MrtSurface(C.Structure):
-    _fields_ = [("kind", C.c_uint32), ("texture", C.c_uint32), ("color", C.c_float * 4)]
+    _fields_ = [("kind", C.c_uint32), ("texture", C.c_uint32), ("color", C.c_float * 4),
+                ("a", C.c_uint32), ("b", C.c_uint32), ("mode", C.c_uint32)]
 
 
 class MrtTexture(C.Structure):
@@ -88,7 +91,8 @@ class MrtTexture(C.Structure):
 
 
 class MrtBackground(C.Structure):
-    _fields_ = [("kind", C.c_uint32), ("surface", C.c_uint32), ("color", C.c_float * 3)]
+    _fields_ = [("kind", C.c_uint32), ("surface", C.c_uint32), ("color", C.c_float * 3),
+                ("faces", C.c_uint32 * 6), ("transform", C.c_float * 16)]
 
 
 class MrtSceneDesc(C.Structure):
@@ -161,6 +165,7 @@ EXPORTED_SYMBOLS = [
     "mrt_reset_kernel_stats", "mrt_selftest_division", "mrt_selftest_slab", "mrt_debug_status", "mrt_debug_build",
     "mrt_builder_new", "mrt_builder_free", "mrt_builder_builtin", "mrt_builder_rand_f32", "mrt_builder_solid",
     "mrt_builder_texture_png", "mrt_builder_texture_rgba", "mrt_builder_material", "mrt_builder_mix", "mrt_builder_add_volume",
+    "mrt_builder_background_cubemap", "mrt_builder_ycbcr", "mrt_builder_blend", "mrt_builder_fallback",
     "mrt_builder_background",
     "mrt_builder_add_sphere", "mrt_builder_add_triangle", "mrt_builder_model", "mrt_builder_model_from_ply",
     "mrt_builder_add_instance", "mrt_builder_camera", "mrt_builder_build_bvh", "mrt_builder_desc",
@@ -214,6 +219,10 @@ def lib() -> C.CDLL:
         "mrt_builder_background": (I, [P, U32, U32, F, F, F]),
         "mrt_builder_mix": (I, [P, F, U32, U32]),
         "mrt_builder_add_volume": (I, [P, fp, F, F, fp]),
+        "mrt_builder_background_cubemap": (I, [P, C.POINTER(C.c_uint32), fp]),
+        "mrt_builder_ycbcr": (I, [P, U32, U32]),
+        "mrt_builder_blend": (I, [P, U32, U32, U32]),
+        "mrt_builder_fallback": (I, [P, F, F, F, F, U32]),
         "mrt_builder_add_sphere": (I, [P, U32, F, F, F, F]),
         "mrt_builder_add_triangle": (I, [P, U32, fp]),
         "mrt_builder_model": (I, [P, U32, U32, fp, U32, I, I]),
@@ -308,6 +317,24 @@ class Builder:
 
     def background(self, kind, surface=0, color=(0.0, 0.0, 0.0)):
         _check_builder(lib().mrt_builder_background(self.h, kind, surface, *color))
+
+    def background_cubemap(self, faces, rotation=(0.0, 0.0, 0.0)):
+        """CubeMap::new(x_pos, x_neg, y_pos, y_neg, z_pos, z_neg, rotation) (material.rs:91-190)."""
+        f = np.ascontiguousarray(faces, dtype=np.uint32).reshape(6)
+        _check_builder(lib().mrt_builder_background_cubemap(self.h, f.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                                            _fptr(_f3(rotation))))
+
+    def ycbcr(self, luma, chroma) -> int:
+        """YCbCrTexture over two texture surfaces (texture.rs:207-250)."""
+        return _check_builder(lib().mrt_builder_ycbcr(self.h, luma, chroma))
+
+    def blend(self, mode, left, right) -> int:
+        """TextureBlend::new(mode, left, right) (texture.rs:303-334)."""
+        return _check_builder(lib().mrt_builder_blend(self.h, mode, left, right))
+
+    def fallback(self, color, surface) -> int:
+        """SolidColorFallback::new(color, surface) (texture.rs:336-357)."""
+        return _check_builder(lib().mrt_builder_fallback(self.h, *[float(c) for c in color], surface))
 
     def add_sphere(self, material, center, radius):
         _check_builder(lib().mrt_builder_add_sphere(self.h, material, *[float(c) for c in center], radius))

@@ -45,6 +45,10 @@ def lib() -> C.CDLL:
         "orc_texture_png": (I, [P, C.c_char_p, U32]),
         "orc_material": (I, [P, U32, U32, F, F, F, F]),
         "orc_background": (I, [P, U32, U32, F, F, F]),
+        "orc_ycbcr": (I, [P, U32, U32]),
+        "orc_blend": (I, [P, U32, U32, U32]),
+        "orc_fallback": (I, [P, F, F, F, F, U32]),
+        "orc_background_cubemap": (I, [P, C.POINTER(C.c_uint32), fp]),
         "orc_mix": (I, [P, F, U32, U32]),
         "orc_add_sphere": (I, [P, U32, F, F, F, F]),
         "orc_add_volume": (I, [P, F, F, F, F, F, F, F, F]),
@@ -175,6 +179,20 @@ class Scene:
 
     def background(self, kind, surface=0, color=(0.0, 0.0, 0.0)):
         self._chk(lib().orc_background(self.h, kind, surface, *color))
+
+    def ycbcr(self, luma, chroma):
+        return self._chk(lib().orc_ycbcr(self.h, luma, chroma))
+
+    def blend(self, mode, left, right):
+        return self._chk(lib().orc_blend(self.h, mode, left, right))
+
+    def fallback(self, color, surface):
+        return self._chk(lib().orc_fallback(self.h, *[float(c) for c in color], surface))
+
+    def background_cubemap(self, faces, rotation=(0.0, 0.0, 0.0)):
+        f = np.ascontiguousarray(faces, dtype=np.uint32).reshape(6)
+        r = np.ascontiguousarray(rotation, dtype=np.float32).reshape(3)
+        self._chk(lib().orc_background_cubemap(self.h, f.ctypes.data_as(C.POINTER(C.c_uint32)), _fp(r)))
 
     def add_sphere(self, material, center, radius):
         self._chk(lib().orc_add_sphere(self.h, material, *[float(c) for c in center], radius))

@@ -45,6 +45,7 @@ static inline V2 operator+(V2 a, V2 b) { return {a.x + b.x, a.y + b.y}; }
 static inline V2 operator-(V2 a, V2 b) { return {a.x - b.x, a.y - b.y}; }
 static inline V2 operator*(V2 a, float s) { return {a.x * s, a.y * s}; }
 static inline V4 operator+(V4 a, V4 b) { return {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
+static inline V4 operator-(V4 a, V4 b) { return {a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w}; }
 static inline V4 operator*(V4 a, float s) { return {a.x * s, a.y * s, a.z * s, a.w * s}; }
 static inline V3 fill(float f) { return {f, f, f}; }
 // generic.rs:8-18
@@ -275,6 +276,48 @@ struct Texture : Surface {  // texture.rs:21-149
   }
 };
 
+// texture.rs:197-250 YCbCrTexture: luma.x, chroma.xy through YUV_TRANSFORM
+// (a point transform), clamped to [0,1], then powf(2.2); alpha 1.
+static const float KR = 0.2126f, KG = 0.7152f, KB = 0.0722f;
+struct YCbCr : Surface {
+  std::shared_ptr<Texture> luma, chroma;
+  V4 get_f(V2 index, Ctx& c) const override {
+    V4 l = luma->get_f(index, c), ch = chroma->get_f(index, c);
+    M4 yuv = mk({1.0f, 1.0f, 1.0f, 0.0f}, {0.0f, -(KB / KG) * (2.0f - 2.0f * KB), 2.0f - 2.0f * KB, 0.0f},
+                {2.0f - 2.0f * KR, -(KR / KG) * (2.0f - 2.0f * KR), 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 1.0f});
+    V3 col = transform(yuv, V3{l.x, ch.x - 0.5f, ch.y - 0.5f}, 1.0f);
+    col = V3{fminf(col.x, 1.0f), fminf(col.y, 1.0f), fminf(col.z, 1.0f)};
+    col = V3{fmaxf(col.x, 0.0f), fmaxf(col.y, 0.0f), fmaxf(col.z, 0.0f)};
+    return V4{powf(col.x, 2.2f), powf(col.y, 2.2f), powf(col.z, 2.2f), 1.0f};
+  }
+};
+// texture.rs:252-267,303-334 TextureBlend: left then right, per-component
+enum { BLEND_LIGHTEN = 0, BLEND_DARKEN = 1, BLEND_ADDITION = 2, BLEND_SUBTRACTION = 3 };
+static V4 vmin4(V4 a, V4 b) { return {fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z), fminf(a.w, b.w)}; }
+static V4 vmax4(V4 a, V4 b) { return {fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w)}; }
+struct Blend : Surface {
+  uint32_t mode;
+  std::shared_ptr<Surface> left, right;
+  V4 get_f(V2 index, Ctx& c) const override {
+    V4 l = left->get_f(index, c), r = right->get_f(index, c);
+    switch (mode) {
+      case BLEND_LIGHTEN: return vmax4(l, r);
+      case BLEND_DARKEN: return vmin4(l, r);
+      case BLEND_ADDITION: return vmin4(l + r, V4{1, 1, 1, 1});
+      default: return vmax4(l - r, V4{0, 0, 0, 0});
+    }
+  }
+};
+// texture.rs:336-357 SolidColorFallback: color*(1-a) + c*a
+struct Fallback : Surface {
+  V4 color;
+  std::shared_ptr<Surface> surface;
+  V4 get_f(V2 index, Ctx& c) const override {
+    V4 v = surface->get_f(index, c);
+    return (color * (1.0f - v.w)) + (v * v.w);
+  }
+};
+
 // ---------------------------------------------------------------- geom.rs Hit
 struct Material;
 struct Hit {  // geom.rs:7-33
@@ -446,6 +489,36 @@ struct SkySphere : Background {  // material.rs:65-89
     float theta = acosf(p.y);
     float phi = atan2f(p.z * -1.0f, p.x) + PI;
     V4 px = tex->get_f(V2{phi / (2.0f * PI), theta / PI}, c);
+    return V3{px.x, px.y, px.z};
+  }
+};
+
+// material.rs:91-190 CubeMap: the direction through `transform` (built from
+// rotate_x three times, material.rs:103-107), the major axis picks the face
+// (ties: x before y before z), uv = 0.5*(u/max+1).
+struct CubeMap : Background {
+  std::shared_ptr<Surface> faces[6];  // x_pos, x_neg, y_pos, y_neg, z_pos, z_neg
+  M4 m;
+  V3 background(const Ray& r, Ctx& c) const override {
+    V3 p = transform(m, r.direction, 0.0f);
+    V3 a{fabsf(p.x), fabsf(p.y), fabsf(p.z)};
+    bool xl = a.x >= a.y && a.x >= a.z, yl = a.y >= a.x && a.y >= a.z, zl = a.z >= a.x && a.z >= a.y;
+    int index = 0;
+    float max_axis = 0.0f, u = 0.0f, v = 0.0f;
+    if (xl) {
+      if (p.x > 0.0f) index = 0, u = p.z * -1.0f, v = p.y;
+      else index = 1, u = p.z, v = p.y;
+      max_axis = a.x;
+    } else if (yl) {
+      if (p.y > 0.0f) index = 3, u = p.x, v = p.z * -1.0f;
+      else index = 2, u = p.x, v = p.z;
+      max_axis = a.y;
+    } else if (zl) {
+      if (p.z > 0.0f) index = 4, u = p.x, v = p.y;
+      else index = 5, u = p.x * -1.0f, v = p.y;
+      max_axis = a.z;
+    }
+    V4 px = faces[index]->get_f(V2{0.5f * (u / max_axis + 1.0f), 0.5f * (v / max_axis + 1.0f)}, c);
     return V3{px.x, px.y, px.z};
   }
 };
@@ -1387,6 +1460,41 @@ int orc_background(orc_scene* s, uint32_t kind, uint32_t surface, float r, float
       s->world.background.reset(new SkyBackground());
     else
       s->world.background.reset(new SkySphere(s->surfaces.at(surface)));
+    return 0;
+  });
+}
+int orc_ycbcr(orc_scene* s, uint32_t luma, uint32_t chroma) {
+  return guard([&] {
+    auto y = std::make_shared<YCbCr>();
+    y->luma = std::dynamic_pointer_cast<Texture>(s->surfaces.at(luma));
+    y->chroma = std::dynamic_pointer_cast<Texture>(s->surfaces.at(chroma));
+    if (!y->luma || !y->chroma) throw std::runtime_error("YCbCr planes must be textures");
+    s->surfaces.push_back(y);
+    return (int)s->surfaces.size() - 1;
+  });
+}
+int orc_blend(orc_scene* s, uint32_t mode, uint32_t left, uint32_t right) {
+  return guard([&] {
+    auto b = std::make_shared<Blend>();
+    b->mode = mode, b->left = s->surfaces.at(left), b->right = s->surfaces.at(right);
+    s->surfaces.push_back(b);
+    return (int)s->surfaces.size() - 1;
+  });
+}
+int orc_fallback(orc_scene* s, float r, float g, float b, float a, uint32_t surface) {
+  return guard([&] {
+    auto f = std::make_shared<Fallback>();
+    f->color = V4{r, g, b, a}, f->surface = s->surfaces.at(surface);
+    s->surfaces.push_back(f);
+    return (int)s->surfaces.size() - 1;
+  });
+}
+int orc_background_cubemap(orc_scene* s, const uint32_t* faces, const float* rotation) {
+  return guard([&] {
+    auto* cm = new CubeMap();
+    for (int k = 0; k < 6; ++k) cm->faces[k] = s->surfaces.at(faces[k]);
+    cm->m = mul(mul(rotate_x(rotation[0]), rotate_x(rotation[1])), rotate_x(rotation[2]));  // material.rs:103-107
+    s->world.background.reset(cm);
     return 0;
   });
 }

@@ -50,6 +50,12 @@ int orc_material(orc_scene* s, uint32_t kind, uint32_t surface, float param, flo
 // through orc_material.
 int orc_mix(orc_scene* s, float ratio, uint32_t left, uint32_t right);
 int orc_background(orc_scene* s, uint32_t kind, uint32_t surface, float r, float g, float b);
+// texture.rs:207-357 composite surfaces; each returns the new surface index
+int orc_ycbcr(orc_scene* s, uint32_t luma, uint32_t chroma);
+int orc_blend(orc_scene* s, uint32_t mode, uint32_t left, uint32_t right);
+int orc_fallback(orc_scene* s, float r, float g, float b, float a, uint32_t surface);
+// material.rs:91-190 CubeMap(x_pos, x_neg, y_pos, y_neg, z_pos, z_neg, rotation)
+int orc_background_cubemap(orc_scene* s, const uint32_t* faces, const float* rotation);
 int orc_add_sphere(orc_scene* s, uint32_t material, float cx, float cy, float cz, float radius);
 // geom.rs:595-653 Volume over a Sphere target with an Isotrophic(albedo) material
 int orc_add_volume(orc_scene* s, float cx, float cy, float cz, float radius, float density, float ar, float ag,

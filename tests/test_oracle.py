@@ -198,3 +198,84 @@ def test_volume_furnace():
     rgb = rgb.reshape(-1, 3)
     assert np.all(rgb == np.round(rgb)) and rgb.max() == spp
     assert b.max() > spp  # multiple scattering inside the medium
+
+
+def _albedo_of_surface(build_surface, W=4, H=3):
+    """Pre-pass albedo of a Lambertian sphere filling the view: the surface's
+    get_f(0,0).xyz (material.rs:205-214 attenuation, world.rs:81-92)."""
+    o = oracle.Scene(1)
+    o.background(massrt.BG_SOLID, 0, (0.0, 0.0, 0.0))
+    s = build_surface(o)
+    o.add_sphere(o.material(massrt.MAT_LAMBERTIAN, s), (0, 0, 0), 100.0)
+    o.build_bvh()
+    o.camera(20.0, (0, 0, 0.5), (0, 0, -1), aspect=1.0)
+    a, _ = o.prepass(W, H, seed=1, threads=1)
+    a = a.reshape(-1, 3)
+    assert np.all(a == a[0])
+    return a[0]
+
+
+@pytest.mark.parametrize("mode", [massrt.BLEND_LIGHTEN, massrt.BLEND_DARKEN, massrt.BLEND_ADDITION,
+                                  massrt.BLEND_SUBTRACTION])
+def test_blend_known_answers(mode):
+    """TextureBlend (texture.rs:252-267,303-334) of two solid colours."""
+    f = np.float32
+    l, r = np.array([0.2, 0.9, 0.5, 1.0], f), np.array([0.6, 0.3, 0.5, 0.5], f)
+    got = _albedo_of_surface(lambda o: o.blend(mode, o.solid(*l), o.solid(*r)))
+    want = {massrt.BLEND_LIGHTEN: np.maximum(l, r), massrt.BLEND_DARKEN: np.minimum(l, r),
+            massrt.BLEND_ADDITION: np.minimum(l + r, f(1)), massrt.BLEND_SUBTRACTION: np.maximum(l - r, f(0))}[mode]
+    assert np.array_equal(got, want[:3])
+
+
+def test_fallback_and_nesting_known_answers():
+    """SolidColorFallback (texture.rs:336-357): color*(1-a) + c*a, nested in a blend."""
+    f = np.float32
+    c, s = np.array([1.0, 0.0, 0.0, 1.0], f), np.array([0.0, 0.0, 1.0, 0.25], f)
+    want = c * (f(1) - s[3]) + s * s[3]
+    assert np.array_equal(_albedo_of_surface(lambda o: o.fallback(c, o.solid(*s))), want[:3])
+    k = np.array([0.1, 0.2, 0.3, 1.0], f)
+    got = _albedo_of_surface(lambda o: o.blend(massrt.BLEND_ADDITION, o.solid(*k), o.fallback(c, o.solid(*s))))
+    assert np.array_equal(got, np.minimum(k + want, f(1))[:3])
+
+
+def test_ycbcr_known_answer():
+    """YCbCrTexture (texture.rs:197-250) of 1x1 planes: BT.709 matrix as a
+    point transform, clamp, powf(2.2)."""
+    f = np.float32
+    luma = np.array([[[200, 0, 0, 255]]], np.uint8)
+    chroma = np.array([[[90, 170, 0, 255]]], np.uint8)
+    got = _albedo_of_surface(lambda o: o.ycbcr(o.texture_rgba(luma, massrt.WRAP_CLAMP),
+                                               o.texture_rgba(chroma, massrt.WRAP_CLAMP)))
+    kr, kg, kb = f(0.2126), f(0.7152), f(0.0722)
+    y, u, v = f(200) / f(255), f(90) / f(255) - f(0.5), f(170) / f(255) - f(0.5)
+    rgb = np.array([y + f(0) * u + (f(2) - f(2) * kr) * v,
+                    y + (-(kb / kg) * (f(2) - f(2) * kb)) * u + (-(kr / kg) * (f(2) - f(2) * kr)) * v,
+                    y + (f(2) - f(2) * kb) * u + f(0) * v], f)
+    want = np.power(np.clip(rgb, f(0), f(1)), f(2.2))
+    assert np.allclose(got, want, rtol=1e-6, atol=0)
+
+
+def test_cubemap_faces():
+    """CubeMap (material.rs:91-190): the major axis of the transformed
+    direction picks the face, +y shows the y_neg face and -y the y_pos face
+    (the reference's index swap), and all three rotation angles act about x."""
+    o = oracle.Scene(1)
+    cols = [(1, 0, 0), (0, 1, 0), (0, 0, 1), (1, 1, 0), (0, 1, 1), (1, 0, 1)]
+    faces = [o.solid(*c, 1.0) for c in cols]  # x_pos x_neg y_pos y_neg z_pos z_neg
+
+    def centre(look_at, rotation=(0, 0, 0)):
+        o.background_cubemap(faces, rotation)
+        o.camera(10.0, (0, 0, 0), look_at, view_up=(0, 0, 1) if look_at[2] == 0 and look_at[0] == 0 else (0, 1, 0),
+                 aspect=1.0)
+        a, _ = o.prepass(3, 3, seed=1, threads=1)
+        return tuple(a.reshape(-1, 3)[4])
+
+    o.add_sphere(o.material(massrt.MAT_LAMBERTIAN, o.solid(1, 1, 1, 1)), (700, 800, 900), 1.0)  # off every axis
+    o.build_bvh()
+    assert centre((1, 0, 0)) == cols[0] and centre((-1, 0, 0)) == cols[1]
+    assert centre((0, 1, 0)) == cols[3] and centre((0, -1, 0)) == cols[2]
+    assert centre((0, 0, 1)) == cols[4] and centre((0, 0, -1)) == cols[5]
+    # a quarter turn about x takes -z to +y (-> the y_neg face); the "y" and
+    # "z" angles rotate about x too
+    for rot in [(0.25, 0, 0), (0, 0.25, 0), (0, 0, 0.25)]:
+        assert centre((0, 0, -1), rot) == cols[3]
