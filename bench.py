@@ -73,10 +73,11 @@ def parse():
 
 
 def asset_dir(scene: str) -> Path:
-    if scene.startswith("mesh"):
+    if scene.startswith("mesh") or scene.startswith("menger"):
         sys.path.insert(0, str(REPO / "tools"))
         from gen_assets import ensure_assets
-        return ensure_assets(REPO / "assets", mesh=True, textures=scene.endswith("textured"))
+        return ensure_assets(REPO / "assets", mesh=scene.startswith("mesh"), textures=scene.endswith("textured"),
+                             environment=scene.startswith("menger"))
     return REPO / "tests" / "golden"
 
 

@@ -5,9 +5,14 @@
 //   mesh_ply     = BASELINE config 4: synthetic 1M-triangle binary PLY + 2 area lights
 //   mesh_obj     = config 4 through obj_loader (v/vt/vn, obj_fns + Lambertian(SolidColor))
 //   mesh_obj_textured = config 5: OBJ mesh + Lambertian(Texture) + SkySphere(Texture)
+//   menger       = Menger::generate       scenes/menger.rs:20-105 (20^5 = 3.2M cube
+//                  instances); menger_l3 = the same with the
+//                  three innermost levels only (8,000 cubes, for quick tests)
 // The scene RNG is the world's wyrand stream (fastrand::seed(1), main.rs:86);
 // draws happen in the same statement order as the Rust scenes.
 #include <stdio.h>
+
+#include <functional>
 
 #include "world.h"
 
@@ -177,6 +182,60 @@ SceneResult mesh_obj(float aspect, const std::string& assets, uint64_t seed, boo
   return r;
 }
 
+// eve::environment (eve.rs:342-364): a CubeMap whose faces are
+// TextureBlend(Addition, stars, YCbCrTexture(luma, chroma)); the stars tile is
+// one shared texture. The PNGs are tools/gen_assets.py stand-ins.
+Background environment(const std::string& assets, const std::string& name, V3 rotation) {
+  SharedTexture stars = Texture::load_png(join_path(assets, "environments/stars01_tile2.png"), WrapMode::Repeat);
+  Surface faces[6];
+  for (int i = 0; i < 6; ++i) {
+    std::string base = join_path(assets, "environments/" + name + "/" + std::to_string(i));
+    Surface nebula = YCbCrTexture(Texture::load_png(base + ".png", WrapMode::Repeat),
+                                  Texture::load_png(base + "_chroma.png", WrapMode::Repeat));
+    faces[i] = TextureBlend(MRT_BLEND_ADDITION, TextureSurface(stars), nebula);
+  }
+  return CubeMap(faces, rotation);
+}
+
+// menger.rs:117-138
+const int MENGER_CUBE_SIDES[20][3] = {{0, 1, 1},   {1, 0, 1},   {1, 1, 0},  {0, -1, -1}, {-1, 0, -1},
+                                      {-1, -1, 0}, {0, -1, 1},  {-1, 0, 1}, {-1, 1, 0},  {0, 1, -1},
+                                      {1, 0, -1},  {1, -1, 0},  {-1, -1, 1}, {-1, 1, -1}, {1, -1, -1},
+                                      {-1, 1, 1},  {1, -1, 1},  {1, 1, -1},  {1, 1, 1},   {-1, -1, -1}};
+
+// menger_gen (menger.rs:69-115): the five nested loops, level k offset by
+// sides * dims * 3^k (f32: (V3 * dims) * powi), innermost added last.
+void menger_gen(World& world, const std::string& assets, int levels) {
+  const float dims = 2.0f;
+  Material material = Lambertian(SolidColor(V4{1, 1, 1, 1}));
+  Model cube = world.model(ply_triangles(join_path(assets, "cube.ply")));
+  float pw[5] = {1.0f, 3.0f, 9.0f, 27.0f, 81.0f};  // (3.0f32).powi(k), exact
+  std::function<void(int, V3)> level = [&](int k, V3 base) {
+    for (const auto& s : MENGER_CUBE_SIDES) {
+      V3 xyz = ((V3{(float)s[0], (float)s[1], (float)s[2]} * dims) * pw[k]) + base;
+      if (k == 0)
+        world.add(cube.instance(xyz, V3{0, 0, 0}, fill3(1.0f)).with_material(material));
+      else
+        level(k - 1, xyz);
+    }
+  };
+  // the outermost loop has no `+ xyz`; adding V3 zero is exact
+  level(levels - 1, V3{0, 0, 0});
+}
+
+SceneResult menger(float aspect, const std::string& assets, uint64_t seed, int levels) {
+  SceneResult r;
+  r.world = std::make_unique<World>(environment(assets, "j02", V3{0.4f, 0.2f, 0.1f}), seed);
+  World& world = *r.world;
+  Model cube = world.model(ply_triangles(join_path(assets, "cube.ply")));
+  Material foggy = Metal(0.7f, SolidColor(V4{0.5f, 0.5f, 0.5f, 1.0f}));
+  menger_gen(world, assets, levels);
+  world.add(cube.instance(V3{0, -244, 0}, V3{0, 0, 0}, V3{500000, 1, 500000}).with_material(foggy));
+  V3 look_from{2680, 140, 2000}, look_at{0, 0, 0};
+  r.camera = Camera::make(15.0f, look_from, look_at, V3{0, 1, 0}, aspect, 0.0f, length(look_from - look_at));
+  return r;
+}
+
 }  // namespace
 
 SceneResult generate_builtin(const std::string& name, float aspect, const std::string& assets, uint64_t seed) {
@@ -193,6 +252,10 @@ SceneResult generate_builtin(const std::string& name, float aspect, const std::s
     r = mesh_obj(aspect, assets, seed, false);
   else if (name == "mesh_obj_textured")
     r = mesh_obj(aspect, assets, seed, true);
+  else if (name == "menger")
+    r = menger(aspect, assets, seed, 5);
+  else if (name == "menger_l3")
+    r = menger(aspect, assets, seed, 3);
   else
     throw Error(MRT_ERR_INVALID, "unknown built-in scene '" + name + "'");
   r.world->build_bvh();  // main.rs:112

@@ -1370,6 +1370,49 @@ static void builtin(orc_scene* s, const std::string& name, float aspect, const s
       add_instance(s, cube, V3{2.5f, 4.0f, 1.0f}, V3{0, 0, 0}, V3{1.0f, 0.0001f, 1.0f}, light);
     }
     cam_at(40.0f, V3{0.0f, 3.2f, 6.5f}, V3{0.0f, -0.2f, 0.0f});
+  } else if (name == "menger" || name == "menger_l3") {  // menger.rs:20-115
+    auto tex = [&](const std::string& path) {
+      std::vector<uint8_t> px;
+      uint32_t w, h;
+      if (!png_rgba(jp(dir, path), px, w, h)) throw std::runtime_error("png " + path);
+      return std::make_shared<Texture>(px.data(), w, h, WRAP_REPEAT);
+    };
+    auto* cm = new CubeMap();  // eve.rs:342-364 environment("j02", (0.4, 0.2, 0.1))
+    auto stars = tex("environments/stars01_tile2.png");
+    for (int f = 0; f < 6; ++f) {
+      auto y = std::make_shared<YCbCr>();
+      std::string base = "environments/j02/" + std::to_string(f);
+      y->luma = tex(base + ".png"), y->chroma = tex(base + "_chroma.png");
+      auto b = std::make_shared<Blend>();
+      b->mode = BLEND_ADDITION, b->left = stars, b->right = y;  // eve.rs:353
+      cm->faces[f] = b;
+    }
+    cm->m = mul(mul(rotate_x(0.4f), rotate_x(0.2f)), rotate_x(0.1f));  // material.rs:103-107
+    s->world.background.reset(cm);
+    int cube = make_model(s, ply_tris(s, jp(dir, "cube.ply"), none), nullptr, false);
+    auto foggy = std::make_shared<Metal>(0.7f, solid(V4{0.5f, 0.5f, 0.5f, 1.0f}));
+    int cube2 = make_model(s, ply_tris(s, jp(dir, "cube.ply"), none), nullptr, false);  // menger_gen's own Model
+    static const int sides[20][3] = {{0, 1, 1},   {1, 0, 1},   {1, 1, 0},   {0, -1, -1}, {-1, 0, -1},
+                                     {-1, -1, 0}, {0, -1, 1},  {-1, 0, 1},  {-1, 1, 0},  {0, 1, -1},
+                                     {1, 0, -1},  {1, -1, 0},  {-1, -1, 1}, {-1, 1, -1}, {1, -1, -1},
+                                     {-1, 1, 1},  {1, -1, 1},  {1, 1, -1},  {1, 1, 1},   {-1, -1, -1}};
+    int levels = name == "menger" ? 5 : 3;
+    // the nested loops of menger_gen as an odometer over the level digits
+    std::vector<int> digit(levels, 0);
+    for (;;) {
+      V3 xyz{0, 0, 0};
+      for (int k = levels - 1; k >= 0; --k) {
+        float p = k == 4 ? 81.0f : k == 3 ? 27.0f : k == 2 ? 9.0f : k == 1 ? 3.0f : 1.0f;
+        const int* sd = sides[digit[levels - 1 - k]];
+        xyz = ((V3{(float)sd[0], (float)sd[1], (float)sd[2]} * 2.0f) * p) + xyz;
+      }
+      add_instance(s, cube2, xyz, V3{0, 0, 0}, fill(1.0f), white);
+      int d = levels - 1;
+      while (d >= 0 && ++digit[d] == 20) digit[d--] = 0;
+      if (d < 0) break;
+    }
+    add_instance(s, cube, V3{0, -244, 0}, V3{0, 0, 0}, V3{500000, 1, 500000}, foggy);
+    cam_at(15.0f, V3{2680, 140, 2000}, V3{0, 0, 0});
   } else {
     throw std::runtime_error("unknown scene " + name);
   }

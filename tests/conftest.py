@@ -30,7 +30,7 @@ def golden_dir():
 @pytest.fixture(scope="session")
 def assets_dir():
     from gen_assets import ensure_assets
-    return ensure_assets(REPO / "assets", mesh=True, textures=True)
+    return ensure_assets(REPO / "assets", mesh=True, textures=True, environment=True)
 
 
 @pytest.fixture(scope="session")

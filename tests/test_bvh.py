@@ -127,3 +127,20 @@ def test_two_items_pop_order():
         first = lst[1][1]
         assert first == (1 if order[1] < order[0] else 0)
         assert_same_tree(b, o)
+
+
+def test_menger_topology(assets_dir):
+    """Menger (menger.rs:20-115): 20^3 cubes node for node; the full 20^5 =
+    3.2M-instance scene by node/instance counts and the
+    number of scene-stream draws (one per BvhNode::new call)."""
+    aspect = float(massrt.ASPECT_RATIO)
+    b = massrt.Builder(1).builtin("menger_l3", aspect, assets_dir)
+    o = oracle.Scene(1).builtin("menger_l3", aspect, assets_dir)
+    d = assert_same_tree(b, o)
+    assert d.n_instances == 8_001 and d.n_nodes == T(8_001) + 2 * T(12)
+    assert np.array_equal(b.desc()[1].fields().view(np.uint32), o.camera_fields().view(np.uint32))
+    b = massrt.Builder(1).builtin("menger", aspect, assets_dir)
+    o = oracle.Scene(1).builtin("menger", aspect, assets_dir)
+    d = b.desc_only()
+    assert d.n_instances == 3_200_001 and d.n_nodes == T(3_200_001) + 2 * T(12) == 4_194_333
+    assert b.rand_f32() == o.rand_f32()

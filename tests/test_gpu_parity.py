@@ -516,3 +516,39 @@ def test_composite_surfaces_and_cubemap_parity(ctx):
     oa, on = o.prepass(64, 36, seed=2)
     assert np.array_equal(gn, on)
     assert np.allclose(ga, oa, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("scene", ["menger_l3", "menger"])
+def test_menger_parity(ctx, assets_dir, scene):
+    """Menger (menger.rs:20-115): cube instances whose faces
+    touch (exact t ties between neighbours, resolved to the later object),
+    a 500000-wide Metal ground instance and a CubeMap of
+    TextureBlend(stars, YCbCr) faces. menger_l3 = 8,000 cubes, full frame;
+    menger = 3.2M instances / 4.19M TLAS nodes, rays + a pixel subset of the
+    1080p frame."""
+    b = massrt.Builder(1).builtin(scene, ASPECT, assets_dir)
+    o = oracle.Scene(1).builtin(scene, ASPECT, assets_dir)
+    ctx.upload(b)
+    _, cam = b.desc()
+    rays = np.concatenate([camera_rays(cam, 20_000, 7), random_rays(4_000, 8, span=400.0)])
+    assert np.array_equal(ctx.trace_rays(rays), o.trace_rays(rays))
+    if scene == "menger_l3":
+        W, H, spp = 64, 36, 2
+        ctx.reset_counters()
+        o.reset_counters()
+        rgb, bo = ctx.render(W, H, 0, spp, seed=31, counters=True)
+        orgb, obo = o.render(W, H, 0, spp, seed=31)
+        assert np.array_equal(bo, obo)
+        assert rel_l2(rgb, orgb) <= RTOL  # YCbCr powf(2.2): ocml vs glibc ULPs
+        gc, oc = ctx.counters(), o.counters()
+        for k in massrt.COUNTER_FIELDS:
+            assert gc[k] == oc[k], (k, gc[k], oc[k])
+    else:
+        W, H, spp = 1920, 1080, 2
+        rgb, bo = ctx.render(W, H, 0, spp, seed=31)
+        px = np.arange(0, W * H, 4999, dtype=np.uint32)
+        orgb, obo = o.render_pixels(W, H, px, 0, spp, seed=31)
+        assert np.array_equal(bo[px], obo)
+        assert rel_l2(rgb.reshape(-1, 3)[px], orgb.reshape(-1, 3)) <= RTOL
+        assert bo.mean() / spp > 1.0  # the sponge and the ground are in view

@@ -9,6 +9,10 @@
   albedo_2048.png      2048^2 RGBA8 albedo (config 5, Lambertian(Texture))
   env_4096x2048.png    4096x2048 RGBA8 equirect sky (config 5, SkySphere; the
                        reference loads 8-bit PNG only, texture.rs:30-69)
+  environments/        stand-in for eve::environment("j02") (eve.rs:342-364, whose
+                       models/environments/ PNGs are not in the reference):
+                       stars01_tile2.png (RGBA star tile) and j02/{0..5}.png (8-bit
+                       grey luma) + j02/{0..5}_chroma.png (RGB chroma), 256x256
 
 Usage: python tools/gen_assets.py [--out assets] [--all]
 """
@@ -119,14 +123,67 @@ def env(w=4096, h=2048):
 
 def write_png(path: Path, rgba: np.ndarray):
     from PIL import Image
-    Image.fromarray(rgba, "RGBA").save(path, compress_level=1)
+    mode = {2: "L", 3: "RGB", 4: "RGBA"}[rgba.ndim if rgba.ndim == 2 else rgba.shape[-1]]
+    Image.fromarray(rgba, mode).save(path, compress_level=1)
 
 
-def ensure_assets(out: Path | str = DEFAULT_DIR, mesh: bool = True, textures: bool = False) -> Path:
+def stars(n=256):
+    """Sparse white/blue-ish points on black (alpha 1): the star tile."""
+    rng = np.random.default_rng(11)
+    img = np.zeros((n, n, 4), dtype=np.uint8)
+    img[..., 3] = 255
+    k = n * n // 180
+    ys, xs = rng.integers(0, n, k), rng.integers(0, n, k)
+    lum = rng.integers(90, 256, k)
+    img[ys, xs, 0] = lum
+    img[ys, xs, 1] = lum
+    img[ys, xs, 2] = np.minimum(255, lum + 30)
+    return img
+
+
+def nebula_face(face: int, n=256):
+    """One cube face of the nebula: smooth value-noise luma (8-bit grey) and
+    chroma (R = Cb+0.5, G = Cr+0.5, B unused) as the YCbCr planes."""
+    rng = np.random.default_rng(100 + face)
+
+    def smooth(cells, amp):
+        g = rng.random((cells + 1, cells + 1))
+        t = np.linspace(0, cells, n, endpoint=False)
+        i = t.astype(int)
+        f = t - i
+        f = f * f * (3 - 2 * f)
+        a = g[i][:, i] * (1 - f)[None, :] + g[i][:, i + 1] * f[None, :]
+        b = g[i + 1][:, i] * (1 - f)[None, :] + g[i + 1][:, i + 1] * f[None, :]
+        return amp * (a * (1 - f)[:, None] + b * f[:, None])
+
+    luma = 0.06 + smooth(4, 0.25) + smooth(12, 0.08)
+    cb = 0.5 + smooth(3, 0.16) - 0.08
+    cr = 0.5 + smooth(5, 0.16) - 0.08
+    l8 = (np.clip(luma, 0, 1) * 255 + 0.5).astype(np.uint8)
+    ch = np.stack([cb, cr, np.full_like(cb, 0.5)], -1)
+    return l8, (np.clip(ch, 0, 1) * 255 + 0.5).astype(np.uint8)
+
+
+def ensure_environment(out: Path, name: str = "j02"):
+    d = out / "environments" / name
+    d.mkdir(parents=True, exist_ok=True)
+    if not (out / "environments" / "stars01_tile2.png").exists():
+        write_png(out / "environments" / "stars01_tile2.png", stars())
+    for f in range(6):
+        if not (d / f"{f}_chroma.png").exists():
+            luma, chroma = nebula_face(f)
+            write_png(d / f"{f}.png", luma)
+            write_png(d / f"{f}_chroma.png", chroma)
+
+
+def ensure_assets(out: Path | str = DEFAULT_DIR, mesh: bool = True, textures: bool = False,
+                  environment: bool = False) -> Path:
     out = Path(out)
     out.mkdir(parents=True, exist_ok=True)
     if not (out / "cube.ply").exists():
         shutil.copy(REPO / "tests" / "golden" / "cube.ply", out / "cube.ply")
+    if environment:
+        ensure_environment(out)
     if mesh and not ((out / "mesh_1m.ply").exists() and (out / "mesh_1m.obj").exists()):
         P, N, UV = torus_grid()
         F = torus_faces()
@@ -147,4 +204,4 @@ if __name__ == "__main__":
     ap.add_argument("--out", default=str(DEFAULT_DIR))
     ap.add_argument("--all", action="store_true")
     a = ap.parse_args()
-    print(ensure_assets(a.out, mesh=True, textures=a.all))
+    print(ensure_assets(a.out, mesh=True, textures=a.all, environment=a.all))
