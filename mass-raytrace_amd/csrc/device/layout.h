@@ -19,6 +19,7 @@
 //   INST   2 slots  {inst_id,blas_begin,blas_end,0} {0,0,0,INST}
 //   MODEL  2 slots  {model_id,blas_begin,blas_end,0} {0,0,0,MODEL}
 //   VOLUME 2 slots  {cx,cy,cz,r}              {volume_id,0,0,VOLUME}  (sphere target)
+//   END    2 slots  {0,0,0,0}                 {0,0,0,END}   closes every region
 // ab = b - a and ac = c - a are precomputed on the host with the same IEEE
 // subtraction Triangle::intersect performs (geom.rs:505-506).
 #pragma once
@@ -27,7 +28,7 @@
 namespace mrt {
 
 enum : uint32_t { KIND_BOX = 1, KIND_SPHERE = 2, KIND_TRI = 3, KIND_INST = 4, KIND_MODEL = 5, KIND_VOLUME = 6 };
-// traversal-only pseudo-kind: the region being traversed has ended (path.h)
+// the region being traversed has ended (record after its last one; path.h)
 constexpr uint32_t KIND_END = 0;
 enum : uint32_t { TRI_FLAG_ALPHA = 1u, TRI_FLAG_UV = 2u };
 

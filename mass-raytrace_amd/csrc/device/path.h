@@ -189,10 +189,13 @@ MRT_DEV float div_cr(float a, const Recip& r) {
   return q;
 }
 // Ray in the space being traversed (world, or an instance's object space)
-// with what the slab test needs: y = RN(1/d) per axis and 1/|d|^2.
+// with what the slab test needs: y = RN(1/d) per axis, the products
+// oy = RN(o*y) of the early slab decision, its error margin om, and |d|^2.
 struct TRay {
   V3 o, d;
   float yx, yy, yz;
+  float oyx, oyy, oyz;  // RN(o.k * y.k)
+  float om;             // max_k |oy.k| * 2^-20 (box_hit_any)
   Recip a;    // |d|^2 for Sphere::intersect
   bool fast;  // every slab quotient of this ray can take div_fast exactly
 };
@@ -216,6 +219,10 @@ MRT_DEV TRay make_tray(V3 o, V3 d, bool scene_fast) {
   r.yx = 1.0f / d.x;
   r.yy = 1.0f / d.y;
   r.yz = 1.0f / d.z;
+  r.oyx = o.x * r.yx;
+  r.oyy = o.y * r.yy;
+  r.oyz = o.z * r.yz;
+  r.om = fmaxf(fmaxf(fabsf(r.oyx), fabsf(r.oyy)), fabsf(r.oyz)) * 0x1p-20f;
   r.a = make_recip(length_squared(d));
   r.fast = scene_fast && coord_ok(o.x) && coord_ok(o.y) && coord_ok(o.z) && dir_ok(d.x) && dir_ok(d.y) &&
            dir_ok(d.z);
@@ -358,7 +365,7 @@ constexpr uint32_t kRetInstance = 0x80000000u;
 struct Trav {
   TRay r;  // ray of the space being traversed (world, or instance object space)
   uint32_t ray;  // pool index of the ray
-  uint32_t i, end, ret;
+  uint32_t i, ret;
   float best;
   uint32_t prim, hit_ret;  // closest hit so far: primitive (kRefNone: none) and `ret` when found
   uint4 s0, s1;  // current record (prefetched when i moves)
@@ -421,21 +428,29 @@ MRT_DEV bool box_hit_exact(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) 
   return !(t1 < t0);
 }
 
-// The same decision, cheaper: in the fast domain each product (m - o)*RN(1/d)
-// is within 2^-21.9 (relative) of the correctly rounded quotient (one rounding
-// in RN(1/d), one in the product, half an ulp to RN(a/d)); min/max keep that
-// bound for t0 and t1 (relative to their own magnitude). When t1 and t0 are
-// further apart than (|t0|+|t1|)*2^-19 the comparison of the exact values is
-// decided; otherwise — grazing rays, flat boxes, ties — box_hit_exact decides.
-// mrt_selftest_slab checks this against box_hit_exact on near-tie boxes.
+// The same decision, cheaper: in the fast domain a = RN(m*y - RN(o*y)) (one
+// FMA per slab plane) is within |Q|*2^-22.4 + |o*y|*2^-23.9 of the correctly
+// rounded quotient RN((m - o)/d) — one rounding in y = RN(1/d), one in o*y,
+// one in the FMA, half an ulp to the quotient; no under/overflow in the fast
+// domain. min/max are 1-Lipschitz and the terms that decide them lie at t0
+// (t1), so t0 and t1 carry that bound relative to their own magnitude plus
+// max_k |o.k*y.k|*2^-23.9. When t1 - t0 exceeds (|t0|+|t1|)*2^-19 + om (om =
+// max_k |o.k*y.k|*2^-20, 4x slack on both terms) the comparison of the exact
+// values is decided; otherwise — grazing rays, flat boxes, ties — the exact
+// test decides. mrt_selftest_slab checks this against box_hit_exact on
+// near-tie boxes.
+MRT_DEV void slab_fast(V3 mn, V3 mx, const TRay& r, float tmin, float tmax, float& t0, float& t1) {
+  const float ax = fmaf(mn.x, r.yx, -r.oyx), ay = fmaf(mn.y, r.yy, -r.oyy), az = fmaf(mn.z, r.yz, -r.oyz);
+  const float bx = fmaf(mx.x, r.yx, -r.oyx), by = fmaf(mx.y, r.yy, -r.oyy), bz = fmaf(mx.z, r.yz, -r.oyz);
+  t0 = vmax3(vmin1(ax, bx), vmin1(ay, by), vmax1(vmin1(az, bz), tmin));
+  t1 = vmin3(vmax1(ax, bx), vmax1(ay, by), vmin1(vmax1(az, bz), tmax));
+}
+MRT_DEV float slab_margin(const TRay& r, float t0, float t1) { return fmaf(fabsf(t0) + fabsf(t1), 0x1p-19f, r.om); }
 MRT_DEV bool box_hit_any(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) {
   if (r.fast) {
-    V3 na = mn - r.o, nb = mx - r.o;
-    const float ax = na.x * r.yx, ay = na.y * r.yy, az = na.z * r.yz;
-    const float bx = nb.x * r.yx, by = nb.y * r.yy, bz = nb.z * r.yz;
-    const float t0 = vmax3(vmin1(ax, bx), vmin1(ay, by), vmax1(vmin1(az, bz), tmin));
-    const float t1 = vmin3(vmax1(ax, bx), vmax1(ay, by), vmin1(vmax1(az, bz), tmax));
-    const float m = (fabsf(t0) + fabsf(t1)) * 0x1p-19f;
+    float t0, t1;
+    slab_fast(mn, mx, r, tmin, tmax, t0, t1);
+    const float m = slab_margin(r, t0, t1);
     const float gap = t1 - t0;
     if (gap > m) return true;
     if (-gap > m) return false;
@@ -448,15 +463,10 @@ MRT_DEV TRay world_ray(const TravIn& in, uint32_t ray) {
   return make_tray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, in.S.fast_ok);
 }
 
-// Load record t.i, or mark the end of the region being traversed with the
-// pseudo-kind KIND_END (handled by trav_prim: leave the BLAS, or finish).
-// Keeping the rare BLAS exit out of this step keeps the box step small.
+// Load record t.i. Every region ends in an END record (handled by
+// trav_prim: leave the BLAS, or finish), so there is no bounds compare here.
 MRT_DEV void trav_fetch(const TravIn& in, Trav& t) {
   const DevScene& S = in.S;
-  if (t.i >= t.end) {
-    t.s1.w = KIND_END;
-    return;
-  }
 #ifdef MRT_DEBUG_BOUNDS
   if (t.i + 1 >= S.n_slots || ++t.steps > (1u << 24)) {  // record and stop instead of looping/faulting
     MRT_IDX(S, t.i + 1 >= S.n_slots ? t.i : 0xFFFFFFF0u, t.i + 1 >= S.n_slots ? S.n_slots : 0u, 5);
@@ -464,8 +474,10 @@ MRT_DEV void trav_fetch(const TravIn& in, Trav& t) {
     return;
   }
 #endif
-  t.s0 = in.slots[MRT_IDX(S, t.i, S.n_slots, 5)];
-  t.s1 = in.slots[MRT_IDX(S, t.i + 1, S.n_slots, 6)];
+  MRT_IDX(S, t.i + 1, S.n_slots, 6);
+  const uint4* p = in.slots + MRT_IDX(S, t.i, S.n_slots, 5);  // one address, offset:16 for slot 2
+  t.s0 = p[0];
+  t.s1 = p[1];
 }
 
 // The region ended: leave the BLAS back to the world ray (geom.rs:405-409;
@@ -478,7 +490,6 @@ MRT_DEV void trav_end(const TravIn& in, Trav& t) {
   }
   if (t.ret & kRetInstance) t.r = world_ray(in, t.ray);
   t.i = t.ret & ~kRetInstance;
-  t.end = in.S.world_end;
   t.ret = kNoRet;
   trav_fetch(in, t);
 }
@@ -494,7 +505,6 @@ MRT_DEV void trav_init(const TravIn& in, Trav& t, uint32_t ray, float tmax) {
   t.r = world_ray(in, ray);
   t.ray = ray;
   t.i = in.S.world_begin;
-  t.end = in.S.world_end;
   t.ret = kNoRet;
   t.best = tmax;
   t.prim = kRefNone;
@@ -597,12 +607,10 @@ MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
     t.r = make_tray(xform(c0, c1, c2, c3, t.r.o, 1.0f), xform(c0, c1, c2, c3, t.r.d, 0.0f), S.fast_ok);
     t.ret = (t.i + 2) | kRetInstance;
     t.i = s0.y;
-    t.end = s0.z;
   } else {  // KIND_MODEL
     if (COUNT) lc.model_entries++;
     t.ret = t.i + 2;
     t.i = s0.y;
-    t.end = s0.z;
   }
   trav_fetch(in, t);
 }

@@ -238,7 +238,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
       // least tune.box_min lanes are at one (lanes reaching a primitive wait)
       for (;;) {
         const bool at_box = !t[q].done && trav_at_box(t[q]);
-        if ((uint32_t)__popcll(__ballot(at_box)) < tune.box_min) break;
+        if ((uint32_t)__popcll(__builtin_amdgcn_ballot_w64(at_box)) < tune.box_min) break;
         if (at_box) trav_box<COUNT>(tin, t[q], lc);
         if (COUNT) {
           lc.wave_slots += lane_id() == 0 ? 64u : 0u;
@@ -721,7 +721,7 @@ __global__ __launch_bounds__(kBlock) void k_selftest_slab(unsigned long long n, 
              (float)((int)(sc >> 24 & 255) - 128) * 0.23f};
     }
     V3 d{dir(rnd()), dir(rnd()), dir(rnd())};
-    const float t = __uint_as_float((uint32_t)(((uint64_t)117u + (rnd() % 20u)) << 23) | ((uint32_t)rnd() & 0x7FFFFFu));
+    const float t = __uint_as_float((uint32_t)(((uint64_t)100u + (rnd() % 37u)) << 23) | ((uint32_t)rnd() & 0x7FFFFFu));
     const V3 p = o + d * t;
     float mn[3], mx[3];
     const float pv[3] = {p.x, p.y, p.z};
@@ -747,12 +747,9 @@ __global__ __launch_bounds__(kBlock) void k_selftest_slab(unsigned long long n, 
     const bool f = box_hit_any(bmn, bmx, ray, tmin, tmax);
     bad += e != f;
     // count how often the exact fallback had to decide
-    V3 na = bmn - ray.o, nb = bmx - ray.o;
-    const float ax = na.x * ray.yx, ay = na.y * ray.yy, az = na.z * ray.yz;
-    const float bx = nb.x * ray.yx, by = nb.y * ray.yy, bz = nb.z * ray.yz;
-    const float t0 = vmax3(vmin1(ax, bx), vmin1(ay, by), vmax1(vmin1(az, bz), tmin));
-    const float t1 = vmin3(vmax1(ax, bx), vmax1(ay, by), vmin1(vmax1(az, bz), tmax));
-    const float m = (fabsf(t0) + fabsf(t1)) * 0x1p-19f;
+    float t0, t1;
+    slab_fast(bmn, bmx, ray, tmin, tmax, t0, t1);
+    const float m = slab_margin(ray, t0, t1);
     ties += !(t1 - t0 > m) && !(t0 - t1 > m);
   }
   bad = (unsigned long long)wave_sum((uint32_t)bad);

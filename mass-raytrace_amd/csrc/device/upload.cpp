@@ -149,6 +149,14 @@ struct Emitter {
     return i;
   }
 
+  // END record closing a region (world or BLAS): a box skip or the last
+  // primitive of the region lands on it, so the device never compares the
+  // record index against the region's end.
+  void push_end() {
+    push_slot(0, 0, 0, 0);
+    push_slot(0, 0, 0, KIND_END);
+  }
+
   bool emit_prim(uint32_t ref, bool in_blas) {
     uint32_t kind = MRT_REF_KIND(ref), idx = MRT_REF_INDEX(ref);
     switch (kind) {
@@ -391,6 +399,7 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
   for (uint32_t r = 0; r < d.n_roots; ++r)
     if (!e.emit_tree(d.roots[r], false)) return false;
   s.world_end = e.n_slots();
+  e.push_end();
   // BLAS regions, one per distinct root, emitted once and shared
   std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> blas;
   for (auto& p : e.jump_patches) {
@@ -399,6 +408,7 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
       uint32_t b = e.n_slots();
       if (!e.emit_tree(MRT_REF(MRT_REF_NODE, p.second), true)) return false;
       it = blas.emplace(p.second, std::make_pair(b, e.n_slots())).first;
+      e.push_end();
     }
     s.slots[4 * p.first + 1] = it->second.first;
     s.slots[4 * p.first + 2] = it->second.second;
