@@ -527,6 +527,15 @@ MRT_DEV void trav_box(const TravIn& in, Trav& t, LocalCounters& lc) {
   trav_fetch(in, t);
 }
 
+// trav_box without the fetch of the next record (k_trace's box run loads at
+// the top of each step).
+template <bool COUNT>
+MRT_DEV void trav_box_index(const TravIn& in, Trav& t, LocalCounters& lc) {
+  if (COUNT) lc.node_visits++;
+  V3 mn{u2f(t.s0.x), u2f(t.s0.y), u2f(t.s0.z)}, mx{u2f(t.s0.w), u2f(t.s1.x), u2f(t.s1.y)};
+  t.i = box_hit_any(mn, mx, t.r, in.tmin, t.best) ? t.i + 2 : t.s1.z;
+}
+
 // The current record is a primitive, an instance or a model. ALPHA=false is
 // the specialisation for scenes without alpha-tested triangles (the alpha
 // test's registers would otherwise cost occupancy everywhere).

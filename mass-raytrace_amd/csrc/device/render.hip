@@ -236,10 +236,14 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
     for (int q = 0; q < R; ++q) {
       // box run: keep stepping boxes with little per-step overhead while at
       // least tune.box_min lanes are at one (lanes reaching a primitive wait)
+      // Every lane (re)loads its record at the top of each step (lanes not
+      // at a box reload the one they hold), so the record registers are
+      // written unconditionally — no merge copies of the held record.
       for (;;) {
+        trav_fetch(tin, t[q]);
         const bool at_box = !t[q].done && trav_at_box(t[q]);
         if ((uint32_t)__popcll(__builtin_amdgcn_ballot_w64(at_box)) < tune.box_min) break;
-        if (at_box) trav_box<COUNT>(tin, t[q], lc);
+        if (at_box) trav_box_index<COUNT>(tin, t[q], lc);
         if (COUNT) {
           lc.wave_slots += lane_id() == 0 ? 64u : 0u;
           lc.lane_steps += at_box ? 1u : 0u;
