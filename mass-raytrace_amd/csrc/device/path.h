@@ -452,6 +452,9 @@ MRT_DEV bool box_hit_any(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) {
     slab_fast(mn, mx, r, tmin, tmax, t0, t1);
     const float m = slab_margin(r, t0, t1);
     const float gap = t1 - t0;
+#ifdef MRT_NO_FALLBACK  // experiment builds only (results NOT exact): cost of the exact fallback
+    return gap >= 0.0f;
+#endif
     if (gap > m) return true;
     if (-gap > m) return false;
   }
@@ -483,7 +486,7 @@ MRT_DEV void trav_fetch(const TravIn& in, Trav& t) {
 // The region ended: leave the BLAS back to the world ray (geom.rs:405-409;
 // a model shares the world ray, an instance's object-space ray is replaced),
 // or finish the ray.
-MRT_DEV void trav_end(const TravIn& in, Trav& t) {
+MRT_DEV void trav_end_index(const TravIn& in, Trav& t) {
   if (t.ret == kNoRet) {
     t.done = true;
     return;
@@ -491,7 +494,6 @@ MRT_DEV void trav_end(const TravIn& in, Trav& t) {
   if (t.ret & kRetInstance) t.r = world_ray(in, t.ray);
   t.i = t.ret & ~kRetInstance;
   t.ret = kNoRet;
-  trav_fetch(in, t);
 }
 
 // Start ray `ray` of the pool (World::intersect(ray, in.tmin, tmax)).
@@ -532,6 +534,10 @@ MRT_DEV void trav_box(const TravIn& in, Trav& t, LocalCounters& lc) {
 template <bool COUNT>
 MRT_DEV void trav_box_index(const TravIn& in, Trav& t, LocalCounters& lc) {
   if (COUNT) lc.node_visits++;
+#ifdef MRT_PAD_VALU  // experiment builds only: VALU sensitivity of the box run
+#pragma unroll
+  for (int k = 0; k < MRT_PAD_VALU; ++k) asm volatile("v_nop");
+#endif
   V3 mn{u2f(t.s0.x), u2f(t.s0.y), u2f(t.s0.z)}, mx{u2f(t.s0.w), u2f(t.s1.x), u2f(t.s1.y)};
   t.i = box_hit_any(mn, mx, t.r, in.tmin, t.best) ? t.i + 2 : t.s1.z;
 }
@@ -569,13 +575,15 @@ MRT_DEV bool volume_hit(const DevScene& S, const TravIn& in, Trav& t, uint4 s0, 
 }
 
 // ALPHA: 0 no alpha tests, 1 alpha tests, 2 alpha tests over EXT surfaces
+// trav_prim_index moves to the next record (or finishes the ray) without
+// loading it; trav_prim also loads it.
 template <bool COUNT, uint32_t ALPHA, bool RNG = false>
-MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
+MRT_DEV void trav_prim_index(const TravIn& in, Trav& t, LocalCounters& lc) {
   const DevScene& S = in.S;
   const uint4 s0 = t.s0, s1 = t.s1;
   const uint32_t kind = s1.w;
   if (kind == KIND_END) {
-    trav_end(in, t);
+    trav_end_index(in, t);
     return;
   }
   if (kind == KIND_TRI) {
@@ -621,7 +629,11 @@ MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
     t.ret = t.i + 2;
     t.i = s0.y;
   }
-  trav_fetch(in, t);
+}
+template <bool COUNT, uint32_t ALPHA, bool RNG = false>
+MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
+  trav_prim_index<COUNT, ALPHA, RNG>(in, t, lc);
+  if (!t.done) trav_fetch(in, t);
 }
 
 // Whole traversal of pool ray `ray` (one ray per thread); RNG: the

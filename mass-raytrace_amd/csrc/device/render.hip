@@ -176,7 +176,7 @@ constexpr uint32_t kIdle = 0xFFFFFFFFu;  // Trav.ray of a lane without a ray
 // (R > 1 would interleave R rays per lane — software ILP; measured slower at
 // its 84 VGPRs, so only R = 1 is instantiated.)
 template <bool COUNT, bool LDS, uint32_t ALPHA, bool RNG>
-__global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ALPHA == 0 && !RNG && !COUNT ? 8 : 1))) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   DevCounters* cnt, float tmin, float tmax, TraceTune tune) {
   constexpr int R = 1;
   extern __shared__ uint4 lds_slots[];
@@ -232,6 +232,32 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
       pool += n_idle < avail ? n_idle : avail;
       if (live == 0) break;  // chunk source exhausted
     }
+#ifdef MRT_UNIFIED_LOOP
+    // Unified steps: every busy lane takes one step — a box test or a
+    // primitive/instance/region-end step — and then every lane that moved
+    // loads its next record with ONE pair of loads (the vector-memory issue
+    // rate, not the ALU, bounds this loop). Repeat until enough lanes have
+    // finished to refill (all of them, once the ray source is drained).
+    const uint32_t need = (pool == pool_end && drained) ? 64u * R : tune.refill * R;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      for (;;) {
+        const bool busy = !t[q].done;  // idle lanes hold a done Trav
+        if (busy) {
+          if (trav_at_box(t[q]))
+            trav_box_index<COUNT>(tin, t[q], lc);
+          else
+            trav_prim_index<COUNT, ALPHA, RNG>(tin, t[q], lc);
+        }
+        if (!t[q].done) trav_fetch(tin, t[q]);
+        if (COUNT) {
+          lc.wave_slots += lane_id() == 0 ? 64u : 0u;
+          lc.lane_steps += busy ? 1u : 0u;
+        }
+        if ((uint32_t)__popcll(__builtin_amdgcn_ballot_w64(t[q].done)) >= need) break;
+      }
+    }
+#else
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       // box run: keep stepping boxes with little per-step overhead while at
@@ -244,10 +270,20 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
         const bool at_box = !t[q].done && trav_at_box(t[q]);
         if ((uint32_t)__popcll(__builtin_amdgcn_ballot_w64(at_box)) < tune.box_min) break;
         if (at_box) trav_box_index<COUNT>(tin, t[q], lc);
+#ifdef MRT_PROBE  // experiment builds: texel_taps = box-run iterations, wave_slots = uniform ones
+        if (COUNT) {
+          const uint32_t f = __builtin_amdgcn_readfirstlane(at_box ? t[q].i : 0xFFFFFFFFu);
+          const bool uni = __builtin_amdgcn_ballot_w64(at_box && t[q].i != f) == 0;
+          lc.texel_taps += lane_id() == 0 ? 1u : 0u;
+          lc.wave_slots += (lane_id() == 0 && uni) ? 1u : 0u;
+          lc.lane_steps += at_box ? 1u : 0u;
+        }
+#else
         if (COUNT) {
           lc.wave_slots += lane_id() == 0 ? 64u : 0u;
           lc.lane_steps += at_box ? 1u : 0u;
         }
+#endif
       }
       const bool busy = !t[q].done;  // idle lanes hold a done Trav
       const bool at_box = busy && trav_at_box(t[q]);
@@ -257,11 +293,17 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, PathBufs in, uint4
       // primitives wait until enough lanes are at one (or no lane is at a box)
       const bool prim_go = (__popcll(prim_mask) >= tune.prim_batch || box_mask == 0) && busy && !at_box;
       if (prim_go) trav_prim<COUNT, ALPHA, RNG>(tin, t[q], lc);
+#ifdef MRT_PROBE
+      if (COUNT) lc.model_entries += lane_id() == 0 ? 1u : 0u;  // outer iterations
+#endif
       if (COUNT) {
+#ifndef MRT_PROBE
         lc.wave_slots += lane_id() == 0 ? 64u : 0u;
+#endif
         lc.lane_steps += (at_box || prim_go) ? 1u : 0u;
       }
     }
+#endif
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       if (t[q].ray != kIdle && t[q].done) {
@@ -823,7 +865,7 @@ struct mrt_ctx {
   // more rays a launch carries the smaller that tail's share (measured on
   // SphereGrid 1080p: 2M paths 186, 16M 377, 64M 434 Msamples/s). 64M paths
   // hold 11 GiB of HBM (176 B each).
-  size_t pool_paths = (size_t)64 << 20;
+  size_t pool_paths = (size_t)128 << 20;
   int cus = 1;
   bool trace_lds = false;          // record stream staged in LDS (set per scene)
 
@@ -889,13 +931,19 @@ void wait_queues(mrt_ctx* c, hipStream_t st) {
 }
 
 // Occupancy-sized persistent grid for kernel f with `smem` dynamic LDS.
-uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem) {
+// `shared`: the kernel runs beside the other queues' kernels (k_trace with
+// several queues) — it takes 3/4 of the occupancy, so another queue's trace
+// and shade launches find room on every CU instead of queueing behind a
+// grid that holds the whole GPU until its last ray (sphere_grid, 2 queues:
+// 8 WGs/CU 585, 6 WGs/CU 618 Msamples/s).
+uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem, bool shared = false) {
   auto key = std::make_pair(f, smem);
   auto it = c->grids.find(key);
   if (it != c->grids.end()) return it->second;
   if (smem > 0) HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTraceLdsMaxBytes));
   int per_cu = 0;
   HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, smem));
+  if (shared) per_cu = std::max(1, per_cu * 3 / 4);
   if (const char* e = getenv("MRT_TRACE_WGS_PER_CU")) per_cu = atoi(e);
   const uint32_t g = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
   c->grids[key] = g;
@@ -907,7 +955,7 @@ void launch_trace_r(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& 
                     float tmin, float tmax) {
   const size_t smem = LDS ? (size_t)c->S.n_slots * 16 : 0;
   const void* f = count ? (const void*)k_trace<true, LDS, ALPHA, RNG> : (const void*)k_trace<false, LDS, ALPHA, RNG>;
-  const uint32_t grid = persistent_grid(c, f, smem);
+  const uint32_t grid = persistent_grid(c, f, smem, c->n_queues > 1);
   if (count)
     hipLaunchKernelGGL((k_trace<true, LDS, ALPHA, RNG>), dim3(grid), dim3(kBlock), smem, st, c->S, in, q.hits,
                        q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
