@@ -233,11 +233,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ALPHA ==
       if (live == 0) break;  // chunk source exhausted
     }
 #ifdef MRT_UNIFIED_LOOP
-    // Unified steps: every busy lane takes one step — a box test or a
-    // primitive/instance/region-end step — and then every lane that moved
-    // loads its next record with ONE pair of loads (the vector-memory issue
-    // rate, not the ALU, bounds this loop). Repeat until enough lanes have
-    // finished to refill (all of them, once the ray source is drained).
+    // Experiment (MRT_UNIFIED_LOOP builds): every busy lane takes one step —
+    // a box test or a primitive/instance/region-end step — and then every
+    // lane that moved loads its next record with ONE pair of loads; repeat
+    // until enough lanes have finished to refill. Utilisation rises (0.60 ->
+    // 0.72) but each iteration runs both the box and the primitive code:
+    // 15-20% slower on sphere_grid / cube_field.
     const uint32_t need = (pool == pool_end && drained) ? 64u * R : tune.refill * R;
 #pragma unroll
     for (int q = 0; q < R; ++q) {
@@ -262,14 +263,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ALPHA ==
     for (int q = 0; q < R; ++q) {
       // box run: keep stepping boxes with little per-step overhead while at
       // least tune.box_min lanes are at one (lanes reaching a primitive wait)
-      // Every lane (re)loads its record at the top of each step (lanes not
-      // at a box reload the one they hold), so the record registers are
-      // written unconditionally — no merge copies of the held record.
       for (;;) {
-        trav_fetch(tin, t[q]);
         const bool at_box = !t[q].done && trav_at_box(t[q]);
-        if ((uint32_t)__popcll(__builtin_amdgcn_ballot_w64(at_box)) < tune.box_min) break;
+        const unsigned long long bm = __builtin_amdgcn_ballot_w64(at_box);
+        if ((uint32_t)__popcll(bm) < tune.box_min) break;
         if (at_box) trav_box_index<COUNT>(tin, t[q], lc);
+        if (at_box) trav_fetch(tin, t[q]);
 #ifdef MRT_PROBE  // experiment builds: texel_taps = box-run iterations, wave_slots = uniform ones
         if (COUNT) {
           const uint32_t f = __builtin_amdgcn_readfirstlane(at_box ? t[q].i : 0xFFFFFFFFu);
