@@ -47,10 +47,16 @@ struct ApiError {
 
 constexpr int kBlock = 256;
 
+// XCD groups: workgroups are dealt round-robin over the 8 XCDs, so
+// blockIdx.x % 8 names the workgroups that share one XCD's L2.
+constexpr uint32_t kGroups = 8;
 struct Ctrl {
   uint32_t active[2];
   uint32_t next_work;
-  uint32_t trace_next;  // persistent k_trace work counter (zeroed by k_shade)
+  uint32_t pad_[29];
+  // persistent k_trace work counters (zeroed by k_shade), one 128-B line per
+  // XCD group: group g takes its rays from the g-th eighth of the pool
+  uint32_t group_next[kGroups * 32];
 };
 
 // SoA path state, 5 x 16 B per slot:
@@ -192,7 +198,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ALPHA ==
   LocalCounters lc;
   uint32_t seg = 0, nh = 0;
   uint32_t pool = 0, pool_end = 0;  // wave-uniform chunk [pool, pool_end)
-  bool drained = false;             // wave-uniform: the counter passed n
+  bool drained = false;             // wave-uniform: every group's share is taken
+  // XCD-aware ray ranges: the pool is roughly in pixel order (camera rays in
+  // tile order, survivors compacted in order), so giving each XCD group a
+  // contiguous eighth keeps an XCD's rays — and the scene parts they touch —
+  // together in that XCD's L2. A group whose eighth is taken helps the next.
+  uint32_t grp = blockIdx.x % kGroups, visited = 0;  // wave-uniform
   Trav t[R];
 #pragma unroll
   for (int q = 0; q < R; ++q) {
@@ -209,13 +220,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ALPHA ==
       n_idle += (uint32_t)__popcll(idle[q]);
     }
     if (n_idle >= tune.refill * R || n_idle == 64u * R) {
-      if (pool == pool_end && !drained) {  // grab the next chunk (wave-uniform)
+      while (pool == pool_end && !drained) {  // grab the next chunk (wave-uniform)
+        const uint32_t lo = (uint32_t)((uint64_t)n * grp / kGroups), hi = (uint32_t)((uint64_t)n * (grp + 1) / kGroups);
         uint32_t b = 0;
-        if (lane_id() == 0) b = atomicAdd(&ctrl->trace_next, tune.chunk);
+        if (lane_id() == 0) b = atomicAdd(&ctrl->group_next[grp * 32], tune.chunk);
         b = __shfl(b, 0, 64);
-        pool = b < n ? b : n;
-        pool_end = b + tune.chunk < n ? b + tune.chunk : n;
-        drained = b + tune.chunk >= n;
+        if (b < hi - lo) {
+          pool = lo + b;
+          pool_end = hi - pool > tune.chunk ? pool + tune.chunk : hi;
+        } else if (++visited == kGroups) {
+          drained = true;
+        } else {
+          grp = (grp + 1) % kGroups;
+        }
       }
       const uint32_t avail = pool_end - pool;
       uint32_t off = 0;
@@ -374,7 +391,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_shade(DevScene S, DevCamera cam, 
                                                   PathBufs out, const uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   uint32_t* work, float4* results, DevCounters* cnt) {
   const uint32_t n = ctrl->active[cur];
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->trace_next = 0;  // k_trace of the next iteration
+  if (blockIdx.x == 0 && threadIdx.x < kGroups) ctrl->group_next[threadIdx.x * 32] = 0;  // next k_trace
   const uint32_t base = blockIdx.x * kBlock;
   if (base >= n) return;
   const uint32_t i = base + threadIdx.x;
