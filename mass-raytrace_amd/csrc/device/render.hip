@@ -387,7 +387,10 @@ MRT_DEV bool shade_step(const DevScene& S, uint32_t max_depth, const Hit& h, V3&
 }
 
 template <bool COUNT, bool EXT>
-__global__ __launch_bounds__(kBlock, 8) void k_shade(DevScene S, DevCamera cam, RenderParams rp, PathBufs in,
+#ifndef MRT_SHADE_WPE
+#define MRT_SHADE_WPE 8
+#endif
+__global__ __launch_bounds__(kBlock, MRT_SHADE_WPE) void k_shade(DevScene S, DevCamera cam, RenderParams rp, PathBufs in,
                                                   PathBufs out, const uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   uint32_t* work, float4* results, DevCounters* cnt) {
   const uint32_t n = ctrl->active[cur];
