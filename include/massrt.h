@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 3
+#define MRT_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 #define MRT_OK 0
@@ -314,7 +314,8 @@ int mrt_builder_free(mrt_builder* b);
 const char* mrt_builder_last_error(void);
 /* Scene::generate of a built-in scene, then World::build_bvh (main.rs:107-112).
  * names: "sphere_grid", "cornell", "cube_field", "mesh_ply", "mesh_obj",
- *        "mesh_obj_textured"; asset_dir holds cube.ply and generated assets. */
+ *        "mesh_obj_textured", "menger", "menger_l3"; asset_dir holds cube.ply
+ *        and generated assets. */
 int mrt_builder_builtin(mrt_builder* b, const char* name, float aspect_ratio, const char* asset_dir);
 float mrt_builder_rand_f32(mrt_builder* b); /* f32::rand() on the scene stream */
 /* surfaces / materials; each returns an index >= 0 */
@@ -352,6 +353,18 @@ int mrt_builder_add_instance(mrt_builder* b, int model, const float* translation
 int mrt_builder_camera(mrt_builder* b, float vfov, const float* look_from, const float* look_at,
                        const float* view_up, float aspect, float aperture, float focus_distance);
 int mrt_builder_build_bvh(mrt_builder* b); /* World::build_bvh (world.rs:117-122) */
+/* World::build_bvh with the top-level tree built on ctx's device
+ * (csrc/device/build.hip): the same nodes, node numbering
+ * and scene-stream draws as mrt_builder_build_bvh (BvhNode::new,
+ * geom.rs:110-161). MRT_ERR_INVALID for a NaN sort key. */
+int mrt_builder_build_bvh_device(mrt_builder* b, mrt_ctx* ctx);
+/* mrt_builder_builtin with the scene's World::build_bvh done on ctx's device */
+int mrt_builder_builtin_device(mrt_builder* b, const char* name, float aspect_ratio, const char* asset_dir,
+                               mrt_ctx* ctx);
+/* wall milliseconds of the builder's last device tree build: host part
+ * (node ranges + axis draws + assembly) and device part (upload, sorts,
+ * boxes, download) */
+int mrt_builder_last_build_ms(mrt_builder* b, double* host_ms, double* device_ms);
 /* flatten; pointers stay valid until the builder is freed or modified */
 int mrt_builder_desc(mrt_builder* b, mrt_scene_desc* desc, mrt_camera* camera);
 

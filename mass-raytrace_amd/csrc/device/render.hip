@@ -1381,6 +1381,12 @@ int mrt_create(int device, mrt_ctx** out) {
   return MRT_OK;
 }
 
+}  // extern "C"
+
+int massrt_ctx_device(const mrt_ctx* c) { return c ? c->device : -1; }
+
+extern "C" {
+
 int mrt_destroy(mrt_ctx* c) {
   if (!c) return MRT_OK;
   hipSetDevice(c->device);

@@ -4,13 +4,18 @@
 // reference-topology tree to the device half as an mrt_scene_desc.
 #include <string.h>
 
+#include "../device/build.h"
 #include "display.h"
 #include "world.h"
+
+// device ordinal of a context (render.hip), -1 for a null context
+int massrt_ctx_device(const mrt_ctx* ctx);
 
 using namespace massrt;
 
 struct mrt_builder {
   std::unique_ptr<World> world;
+  DeviceBuildStats build_stats;
   Camera camera;
   bool has_camera = false;
   std::vector<Model> models;
@@ -288,6 +293,43 @@ int mrt_builder_camera(mrt_builder* b, float vfov, const float* from, const floa
     b->has_camera = true;
     return 0;
   });
+}
+
+static TreeBuilder device_builder(mrt_builder* b, mrt_ctx* ctx) {
+  const int device = massrt_ctx_device(ctx);
+  if (device < 0) throw Error(MRT_ERR_INVALID, "null device context");
+  return [b, device](const std::vector<Item>& items, mrt::WyRand& rng, std::vector<mrt_node>& nodes,
+                     BoundingBox& root_box) { device_build_tree(device, items, rng, nodes, root_box, &b->build_stats); };
+}
+
+int mrt_builder_build_bvh_device(mrt_builder* b, mrt_ctx* ctx) {
+  int rc = guard(b, [&] {
+    b->world->build_bvh(device_builder(b, ctx));
+    return 0;
+  });
+  return rc < 0 ? -rc : rc;
+}
+
+int mrt_builder_builtin_device(mrt_builder* b, const char* name, float aspect, const char* asset_dir, mrt_ctx* ctx) {
+  int rc = guard(b, [&] {
+    const TreeBuilder tb = device_builder(b, ctx);
+    uint64_t seed = b->world->rng.state;
+    SceneResult r = generate_builtin(name ? name : "", aspect, asset_dir ? asset_dir : "", seed, &tb);
+    b->world = std::move(r.world);
+    b->camera = r.camera;
+    b->has_camera = true;
+    return 0;
+  });
+  return rc < 0 ? -rc : rc;
+}
+
+int mrt_builder_last_build_ms(mrt_builder* b, double* host_ms, double* device_ms) {
+  int rc = guard(b, [&] {
+    if (host_ms) *host_ms = b->build_stats.host_ms;
+    if (device_ms) *device_ms = b->build_stats.device_ms;
+    return 0;
+  });
+  return rc < 0 ? -rc : rc;
 }
 
 int mrt_builder_build_bvh(mrt_builder* b) {

@@ -238,7 +238,8 @@ SceneResult menger(float aspect, const std::string& assets, uint64_t seed, int l
 
 }  // namespace
 
-SceneResult generate_builtin(const std::string& name, float aspect, const std::string& assets, uint64_t seed) {
+SceneResult generate_builtin(const std::string& name, float aspect, const std::string& assets, uint64_t seed,
+                             const TreeBuilder* top_level) {
   SceneResult r;
   if (name == "sphere_grid")
     r = sphere_grid(aspect, assets, seed);
@@ -258,7 +259,10 @@ SceneResult generate_builtin(const std::string& name, float aspect, const std::s
     r = menger(aspect, assets, seed, 3);
   else
     throw Error(MRT_ERR_INVALID, "unknown built-in scene '" + name + "'");
-  r.world->build_bvh();  // main.rs:112
+  if (top_level)
+    r.world->build_bvh(*top_level);  // the same tree, built on the device (build.hip)
+  else
+    r.world->build_bvh();  // main.rs:112
   return r;
 }
 

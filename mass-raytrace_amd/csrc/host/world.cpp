@@ -349,6 +349,20 @@ void World::build_bvh() {
   objects_.push_back(Item{MRT_REF(MRT_REF_NODE, root), box});
 }
 
+void World::build_bvh(const TreeBuilder& builder) {
+  std::vector<Item> items = std::move(objects_);
+  objects_.clear();
+  const uint32_t root = (uint32_t)nodes_.size();
+  BoundingBox box;
+  try {
+    builder(items, rng, nodes_, box);
+  } catch (...) {
+    objects_ = std::move(items);  // the world is unchanged by a failed build
+    throw;
+  }
+  objects_.push_back(Item{MRT_REF(MRT_REF_NODE, root), box});
+}
+
 const mrt_scene_desc& World::desc() {
   roots_.clear();
   for (const Item& it : objects_) roots_.push_back(it.ref);

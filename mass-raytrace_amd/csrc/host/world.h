@@ -285,6 +285,13 @@ struct Camera {  // world.rs:5-51
 
 // World<B>: background + object list; owns the typed arrays behind every
 // reference, including all BLAS nodes of models created against it.
+// Builds the tree over a World's objects somewhere else (the device builder,
+// csrc/device/build.hip): appends to `nodes` exactly what World::bvh_new
+// would (preorder numbering from nodes.size(), one rng.axis() per node) and
+// returns the root's box.
+using TreeBuilder =
+    std::function<void(const std::vector<Item>& items, mrt::WyRand& rng, std::vector<mrt_node>& nodes, BoundingBox& root_box)>;
+
 class World {
  public:
   explicit World(Background bg, uint64_t rng_seed = 1) : background_(std::move(bg)) { rng.state = rng_seed; }
@@ -301,6 +308,7 @@ class World {
   Model model(std::vector<Triangle> triangles);
   Model model_with_material(Material m, std::vector<Triangle> triangles);
   void build_bvh();  // world.rs:117-122
+  void build_bvh(const TreeBuilder& builder);  // the same tree, built by `builder`
 
   void set_background(Background bg) { background_ = std::move(bg); }
   // flatten into the C ABI description (pointers valid until modified)
@@ -363,6 +371,6 @@ struct SceneResult {
 };
 // Scene::generate + World::build_bvh for a built-in scene.
 SceneResult generate_builtin(const std::string& name, float aspect_ratio, const std::string& asset_dir,
-                             uint64_t seed);
+                             uint64_t seed, const TreeBuilder* top_level = nullptr);
 
 }  // namespace massrt

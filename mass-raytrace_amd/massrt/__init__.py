@@ -26,7 +26,7 @@ LIB_PATH = (Path(_SEL) if _SEL.endswith(".so") else
 REPO = _HERE.parent.parent
 
 # ---- constants (massrt.h) --------------------------------------------------
-ABI_VERSION = 3  # MRT_ABI_VERSION this binding was written for
+ABI_VERSION = 4  # MRT_ABI_VERSION this binding was written for
 REF_NONE, REF_NODE, REF_SPHERE, REF_TRIANGLE, REF_INSTANCE, REF_MODEL, REF_VOLUME = range(7)
 MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_SPECULAR, MAT_ISOTROPHIC, MAT_MIX = range(8)
 WRAP_MIRROR, WRAP_REPEAT, WRAP_CLAMP = range(3)
@@ -169,6 +169,7 @@ EXPORTED_SYMBOLS = [
     "mrt_builder_background",
     "mrt_builder_add_sphere", "mrt_builder_add_triangle", "mrt_builder_model", "mrt_builder_model_from_ply",
     "mrt_builder_add_instance", "mrt_builder_camera", "mrt_builder_build_bvh", "mrt_builder_desc",
+    "mrt_builder_build_bvh_device", "mrt_builder_builtin_device", "mrt_builder_last_build_ms",
     "mrt_builder_last_error", "mrt_load_ply", "mrt_load_stl", "mrt_load_obj",
     "mrt_tonemap_device", "mrt_tonemap", "mrt_write_png", "mrt_display_gamma_thresholds",
     "mrt_prepass_device", "mrt_prepass",
@@ -230,6 +231,9 @@ def lib() -> C.CDLL:
         "mrt_builder_add_instance": (I, [P, I, fp, fp, fp, U32]),
         "mrt_builder_camera": (I, [P, F, fp, fp, fp, F, F, F]),
         "mrt_builder_build_bvh": (I, [P]),
+        "mrt_builder_build_bvh_device": (I, [P, P]),
+        "mrt_builder_builtin_device": (I, [P, C.c_char_p, F, C.c_char_p, P]),
+        "mrt_builder_last_build_ms": (I, [P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
         "mrt_builder_desc": (I, [P, C.POINTER(MrtSceneDesc), C.POINTER(MrtCamera)]),
         "mrt_load_ply": (I64, [C.c_char_p, fp, U64]),
         "mrt_load_stl": (I64, [C.c_char_p, fp, U64]),
@@ -293,6 +297,23 @@ class Builder:
         if rc != 0:
             raise MassrtError(lib().mrt_builder_last_error().decode())
         return self
+
+    def builtin_device(self, name: str, ctx: "Context", aspect: float = float(ASPECT_RATIO),
+                       asset_dir: str | os.PathLike = ""):
+        """builtin() with World::build_bvh done on ctx's GPU (same tree)."""
+        rc = lib().mrt_builder_builtin_device(self.h, name.encode(), aspect, str(asset_dir).encode(), ctx.h)
+        if rc != 0:
+            raise MassrtError(lib().mrt_builder_last_error().decode())
+        return self
+
+    def build_bvh_device(self, ctx: "Context"):
+        if lib().mrt_builder_build_bvh_device(self.h, ctx.h) != 0:
+            raise MassrtError(lib().mrt_builder_last_error().decode())
+
+    def last_build_ms(self):
+        h, d = C.c_double(), C.c_double()
+        lib().mrt_builder_last_build_ms(self.h, C.byref(h), C.byref(d))
+        return h.value, d.value
 
     def rand_f32(self) -> float:
         return lib().mrt_builder_rand_f32(self.h)

@@ -76,8 +76,9 @@ def test_mesh_scene_topology(name, assets_dir):
     assert sum(1 for x in l2 if x[0] == 1) == T(1_000_000)
 
 
-def random_world(seed, n_spheres, ties):
-    """Same random world built through both builders."""
+def random_world(seed, n_spheres, ties, ctx=None):
+    """Same random world built through both builders (the product's top-level
+    tree on ctx's device when ctx is given, build.hip)."""
     rng = np.random.default_rng(seed)
     b, o = massrt.Builder(seed), oracle.Scene(seed)
     sb, so = b.solid(0.5, 0.5, 0.5), o.solid(0.5, 0.5, 0.5)
@@ -98,7 +99,10 @@ def random_world(seed, n_spheres, ties):
             tri = rng.integers(-2, 2, size=9).astype(np.float32) if ties else rng.normal(size=9).astype(np.float32)
             b.add_triangle(mb, tri)
             o.add_triangle(mo, tri)
-    b.build_bvh()
+    if ctx is None:
+        b.build_bvh()
+    else:
+        b.build_bvh_device(ctx)
     o.build_bvh()
     return b, o
 
@@ -144,3 +148,40 @@ def test_menger_topology(assets_dir):
     d = b.desc_only()
     assert d.n_instances == 3_200_001 and d.n_nodes == T(3_200_001) + 2 * T(12) == 4_194_333
     assert b.rand_f32() == o.rand_f32()
+
+
+def test_device_build_needs_context():
+    b = massrt.Builder(1)
+    m = b.material(massrt.MAT_LAMBERTIAN, b.solid(1, 1, 1))
+    b.add_sphere(m, (0, 0, 0), 1.0)
+    assert massrt.lib().mrt_builder_build_bvh_device(b.h, None) != 0
+
+
+# ---- device tree build (csrc/device/build.hip): the same tree, node for node
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,n,ties", [(1, 1, False), (2, 2, False), (3, 3, True), (4, 64, True),
+                                         (5, 333, False), (6, 1000, True), (7, 20_000, False),
+                                         (8, 20_000, True)])
+def test_device_build_random_worlds(ctx, seed, n, ties):
+    b, o = random_world(seed, n, ties, ctx=ctx)
+    assert_same_tree(b, o)
+    assert b.rand_f32() == o.rand_f32()  # same number of scene-stream draws
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cornell", "sphere_grid", "cube_field", "menger"])
+def test_device_build_builtin_scenes(ctx, name, assets_dir):
+    aspect = float(massrt.ASPECT_RATIO)
+    h = massrt.Builder(1).builtin(name, aspect, assets_dir)
+    b = massrt.Builder(1).builtin_device(name, ctx, aspect, assets_dir)
+    lh, bh = massrt.preorder(h.desc_only())
+    lb, bb = massrt.preorder(b.desc_only())
+    assert lh == lb
+    ph = np.array([x for x in bh if x is not None], dtype=np.float32)
+    pd = np.array([x for x in bb if x is not None], dtype=np.float32)
+    assert np.array_equal(ph.view(np.uint32), pd.view(np.uint32))
+    assert h.rand_f32() == b.rand_f32()
+    host_ms, dev_ms = b.last_build_ms()
+    assert host_ms >= 0 and dev_ms > 0
