@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 4
+#define MRT_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
 #define MRT_OK 0
@@ -273,7 +273,8 @@ int mrt_upload_scene(mrt_ctx* ctx, const mrt_scene_desc* scene);
 int mrt_set_camera(mrt_ctx* ctx, const mrt_camera* camera);
 /* host buffers: accum_rgb = width*height*3 floats, accum_bounces = width*height */
 int mrt_render(mrt_ctx* ctx, const mrt_render_args* args, float* accum_rgb, uint32_t* accum_bounces);
-/* device buffers, enqueued on `hip_stream` (hipStream_t, may be NULL) */
+/* device buffers, enqueued on `hip_stream` (hipStream_t; NULL = the null stream, ordered
+ * with the caller's default-stream work) */
 int mrt_render_device(mrt_ctx* ctx, const mrt_render_args* args, float* d_accum_rgb,
                       uint32_t* d_accum_bounces, void* hip_stream);
 /* rays: n x {ox,oy,oz,dx,dy,dz} host floats; out: n hits. Draws during the
@@ -300,6 +301,26 @@ int mrt_debug_build(void);
 int mrt_reset_kernel_stats(mrt_ctx* ctx);
 /* bytes of device memory held for the scene */
 int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
+
+/* ---- multi-GPU tile exchange (Image::merge, main.rs:629-638) ------------
+ * A render sharded over N devices (mrt_render_args.shard_index/count) leaves
+ * each device's accumulation buffers holding its own tiles only. A shard's
+ * SLAB packs exactly those pixels, in the order the shard owns them (tiles
+ * t = shard_index, shard_index + shard_count, ... in raster order of 8x8
+ * tiles, pixels of a tile in raster order), 16 B per pixel:
+ * {r, g, b, bounces as u32 bits}. Gathering every shard's slab to one
+ * device (RCCL send/recv or a peer copy) and unpacking them there yields the
+ * 1-device image bit for bit: every pixel is summed on one device only.
+ * mrt_shard_pixels is host-only (no device); pixels may be NULL to count. */
+int mrt_shard_pixels(uint32_t width, uint32_t height, uint32_t shard_index, uint32_t shard_count,
+                     uint32_t* pixels, uint32_t* count);
+/* d_slab: count*4 words (device), enqueued on `hip_stream` */
+int mrt_shard_pack_device(mrt_ctx* ctx, uint32_t width, uint32_t height, uint32_t shard_index, uint32_t shard_count,
+                          const float* d_accum_rgb, const uint32_t* d_accum_bounces, void* d_slab, void* hip_stream);
+/* overwrites the shard's pixels of the accumulation buffers with the slab */
+int mrt_shard_unpack_device(mrt_ctx* ctx, uint32_t width, uint32_t height, uint32_t shard_index,
+                            uint32_t shard_count, const void* d_slab, float* d_accum_rgb, uint32_t* d_accum_bounces,
+                            void* hip_stream);
 
 /* ---- host scene builder (C++ mirror of the reference trait surface) -----
  * A builder owns a World under construction plus the scene RNG (fastrand

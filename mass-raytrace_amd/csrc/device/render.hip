@@ -691,6 +691,27 @@ __global__ __launch_bounds__(kBlock) void k_max_u32(const uint32_t* v, uint32_t 
   if (lane_id() == 0) atomicMax(out, m);
 }
 
+// Tile-slab exchange (mrt_shard_*): slab k = the shard's k-th pixel.
+__global__ __launch_bounds__(kBlock) void k_shard_pack(const uint32_t* pixlist, uint32_t n, const float* rgb,
+                                                       const uint32_t* b, uint4* slab) {
+  const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t p = pixlist[k];
+  slab[k] = make_uint4(__float_as_uint(rgb[3 * (size_t)p]), __float_as_uint(rgb[3 * (size_t)p + 1]),
+                       __float_as_uint(rgb[3 * (size_t)p + 2]), b[p]);
+}
+__global__ __launch_bounds__(kBlock) void k_shard_unpack(const uint32_t* pixlist, uint32_t n, const uint4* slab,
+                                                         float* rgb, uint32_t* b) {
+  const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t p = pixlist[k];
+  const uint4 v = slab[k];
+  rgb[3 * (size_t)p] = __uint_as_float(v.x);
+  rgb[3 * (size_t)p + 1] = __uint_as_float(v.y);
+  rgb[3 * (size_t)p + 2] = __uint_as_float(v.z);
+  b[p] = v.w;
+}
+
 // Camera::albedo_normal for pixel p (one ray, no jitter). The rays go through
 // ray_ro/ray_rd so that the traversal can re-read them (TravIn).
 template <bool RNG, bool EXT>
@@ -1062,12 +1083,9 @@ void ensure_slots(mrt_ctx* c, size_t n) {
   c->slots_cap = n;
 }
 
-std::pair<uint32_t*, uint32_t> pixlist(mrt_ctx* c, uint32_t W, uint32_t H, uint32_t si, uint32_t sc) {
-  auto key = std::make_tuple(W, H, si, sc);
-  auto it = c->pixlists.find(key);
-  if (it != c->pixlists.end()) return it->second;
-  // MRT_TILE x MRT_TILE tiles in raster order; this shard owns t % sc == si;
-  // pixels of a tile in raster order, y = 0 the bottom row (main.rs:253-263)
+// MRT_TILE x MRT_TILE tiles in raster order; shard si of sc owns t % sc == si;
+// pixels of a tile in raster order, y = 0 the bottom row (main.rs:253-263)
+std::vector<uint32_t> shard_pixel_list(uint32_t W, uint32_t H, uint32_t si, uint32_t sc) {
   uint32_t tx = (W + MRT_TILE - 1) / MRT_TILE, ty = (H + MRT_TILE - 1) / MRT_TILE;
   std::vector<uint32_t> list;
   for (uint32_t t = si; t < tx * ty; t += sc) {
@@ -1078,6 +1096,14 @@ std::pair<uint32_t*, uint32_t> pixlist(mrt_ctx* c, uint32_t W, uint32_t H, uint3
         if (x < W && y < H) list.push_back(y * W + x);
       }
   }
+  return list;
+}
+
+std::pair<uint32_t*, uint32_t> pixlist(mrt_ctx* c, uint32_t W, uint32_t H, uint32_t si, uint32_t sc) {
+  auto key = std::make_tuple(W, H, si, sc);
+  auto it = c->pixlists.find(key);
+  if (it != c->pixlists.end()) return it->second;
+  const std::vector<uint32_t> list = shard_pixel_list(W, H, si, sc);
   uint32_t* d = nullptr;
   if (!list.empty()) {
     HIP_CHECK(hipMalloc(&d, list.size() * 4));
@@ -1544,7 +1570,7 @@ int mrt_set_camera(mrt_ctx* c, const mrt_camera* cam) {
 int mrt_render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t* d_b, void* stream) {
   return guarded(c, [&] {
     if (!d_rgb || !d_b) throw ApiError{MRT_ERR_INVALID, "null accumulation buffer"};
-    render_device(c, a, d_rgb, d_b, stream ? (hipStream_t)stream : c->stream);
+    render_device(c, a, d_rgb, d_b, (hipStream_t)stream);  // NULL: the null stream
   });
 }
 
@@ -1669,7 +1695,7 @@ int mrt_tonemap_device(mrt_ctx* c, uint32_t W, uint32_t H, const float* d_rgb, c
     if (!d_out || (aux && !d_rgb) ||
         (passes && ((mode == MRT_DISPLAY_DEFAULT && !d_rgb) || (mode == MRT_DISPLAY_DEPTH && !d_b))))
       throw ApiError{MRT_ERR_INVALID, "null buffer"};
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t st = (hipStream_t)stream;  // NULL: the null stream (ordered with the caller's default-stream work)
     const uint32_t n = W * H;
     if (!c->gamma_d) {
       HIP_CHECK(hipMalloc(&c->gamma_d, 256 * 4));
@@ -1718,7 +1744,7 @@ int mrt_prepass_device(mrt_ctx* c, uint32_t W, uint32_t H, uint64_t seed, float*
     if (!c->has_camera) throw ApiError{MRT_ERR_STATE, "no camera set"};
     if (W == 0 || H == 0 || (uint64_t)W * H >= (1ull << 32)) throw ApiError{MRT_ERR_INVALID, "bad image size"};
     if (!d_albedo || !d_normal) throw ApiError{MRT_ERR_INVALID, "null buffer"};
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t st = (hipStream_t)stream;  // NULL: the null stream (ordered with the caller's default-stream work)
     wait_queues(c, st);
     const uint32_t n = W * H;
     ensure_slots(c, n);  // the pre-pass rays
@@ -1781,6 +1807,58 @@ int mrt_debug_build(void) {
 #else
   return 0;
 #endif
+}
+
+int mrt_shard_pixels(uint32_t W, uint32_t H, uint32_t si, uint32_t sc, uint32_t* pixels, uint32_t* count) {
+  try {
+    if (!count) throw ApiError{MRT_ERR_INVALID, "null count"};
+    if (W == 0 || H == 0 || (uint64_t)W * H >= (1ull << 32)) throw ApiError{MRT_ERR_INVALID, "bad image size"};
+    if (sc == 0) sc = 1;
+    if (si >= sc) throw ApiError{MRT_ERR_INVALID, "shard_index >= shard_count"};
+    const std::vector<uint32_t> list = shard_pixel_list(W, H, si, sc);
+    *count = (uint32_t)list.size();
+    if (pixels && !list.empty()) memcpy(pixels, list.data(), list.size() * 4);
+    return MRT_OK;
+  } catch (const ApiError& e) {
+    g_last_error = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_last_error = "out of host memory";
+    return MRT_ERR_NOMEM;
+  }
+}
+
+static int shard_exchange(mrt_ctx* c, uint32_t W, uint32_t H, uint32_t si, uint32_t sc, const void* src_rgb,
+                          const void* src_b, const void* slab, float* dst_rgb, uint32_t* dst_b, void* stream,
+                          bool pack) {
+  return guarded(c, [&] {
+    if (W == 0 || H == 0 || (uint64_t)W * H >= (1ull << 32)) throw ApiError{MRT_ERR_INVALID, "bad image size"};
+    if (sc == 0) sc = 1;
+    if (si >= sc) throw ApiError{MRT_ERR_INVALID, "shard_index >= shard_count"};
+    if (!slab || (pack && (!src_rgb || !src_b)) || (!pack && (!dst_rgb || !dst_b)))
+      throw ApiError{MRT_ERR_INVALID, "null buffer"};
+    hipStream_t st = (hipStream_t)stream;  // NULL: the null stream (ordered with the caller's default-stream work)
+    auto pl = pixlist(c, W, H, si, sc);
+    if (pl.second == 0) return;
+    const dim3 grid((pl.second + kBlock - 1) / kBlock);
+    if (pack)
+      hipLaunchKernelGGL(k_shard_pack, grid, dim3(kBlock), 0, st, pl.first, pl.second, (const float*)src_rgb,
+                         (const uint32_t*)src_b, (uint4*)slab);
+    else
+      hipLaunchKernelGGL(k_shard_unpack, grid, dim3(kBlock), 0, st, pl.first, pl.second, (const uint4*)slab, dst_rgb,
+                         dst_b);
+    HIP_CHECK(hipGetLastError());
+  });
+}
+
+int mrt_shard_pack_device(mrt_ctx* c, uint32_t W, uint32_t H, uint32_t si, uint32_t sc, const float* d_rgb,
+                          const uint32_t* d_b, void* d_slab, void* stream) {
+  return shard_exchange(c, W, H, si, sc, d_rgb, d_b, d_slab, nullptr, nullptr, stream, true);
+}
+
+int mrt_shard_unpack_device(mrt_ctx* c, uint32_t W, uint32_t H, uint32_t si, uint32_t sc, const void* d_slab,
+                            float* d_rgb, uint32_t* d_b, void* stream) {
+  return shard_exchange(c, W, H, si, sc, nullptr, nullptr, d_slab, d_rgb, d_b, stream, false);
 }
 
 int mrt_reset_counters(mrt_ctx* c) {

@@ -26,7 +26,7 @@ LIB_PATH = (Path(_SEL) if _SEL.endswith(".so") else
 REPO = _HERE.parent.parent
 
 # ---- constants (massrt.h) --------------------------------------------------
-ABI_VERSION = 4  # MRT_ABI_VERSION this binding was written for
+ABI_VERSION = 5  # MRT_ABI_VERSION this binding was written for
 REF_NONE, REF_NODE, REF_SPHERE, REF_TRIANGLE, REF_INSTANCE, REF_MODEL, REF_VOLUME = range(7)
 MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_SPECULAR, MAT_ISOTROPHIC, MAT_MIX = range(8)
 WRAP_MIRROR, WRAP_REPEAT, WRAP_CLAMP = range(3)
@@ -173,6 +173,7 @@ EXPORTED_SYMBOLS = [
     "mrt_builder_last_error", "mrt_load_ply", "mrt_load_stl", "mrt_load_obj",
     "mrt_tonemap_device", "mrt_tonemap", "mrt_write_png", "mrt_display_gamma_thresholds",
     "mrt_prepass_device", "mrt_prepass",
+    "mrt_shard_pixels", "mrt_shard_pack_device", "mrt_shard_unpack_device",
 ]
 
 _lib = None
@@ -244,6 +245,9 @@ def lib() -> C.CDLL:
         "mrt_display_gamma_thresholds": (I, [C.POINTER(C.c_uint32)]),
         "mrt_prepass_device": (I, [P, U32, U32, U64, P, P, P]),
         "mrt_prepass": (I, [P, U32, U32, U64, fp, fp]),
+        "mrt_shard_pixels": (I, [U32, U32, U32, U32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+        "mrt_shard_pack_device": (I, [P, U32, U32, U32, U32, P, P, P, P]),
+        "mrt_shard_unpack_device": (I, [P, U32, U32, U32, U32, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -563,6 +567,32 @@ class Context:
 
     def reset_kernel_stats(self):
         self._check(lib().mrt_reset_kernel_stats(self.h))
+
+    def shard_pack_device(self, width, height, shard_index, shard_count, d_rgb: int, d_bounces: int, d_slab: int,
+                          stream: int | None = None):
+        """This shard's pixels of the accumulation buffers -> slab (16 B per pixel)."""
+        self._check(lib().mrt_shard_pack_device(self.h, width, height, shard_index, shard_count, C.c_void_p(d_rgb),
+                                                C.c_void_p(d_bounces), C.c_void_p(d_slab), C.c_void_p(stream or 0)))
+
+    def shard_unpack_device(self, width, height, shard_index, shard_count, d_slab: int, d_rgb: int, d_bounces: int,
+                            stream: int | None = None):
+        """Slab -> this shard's pixels of the accumulation buffers (overwritten)."""
+        self._check(lib().mrt_shard_unpack_device(self.h, width, height, shard_index, shard_count, C.c_void_p(d_slab),
+                                                  C.c_void_p(d_rgb), C.c_void_p(d_bounces), C.c_void_p(stream or 0)))
+
+
+def shard_pixels(width: int, height: int, shard_index: int, shard_count: int) -> np.ndarray:
+    """Pixel indices (p = y*W + x) shard `shard_index` of `shard_count` owns, in slab order (host only)."""
+    n = C.c_uint32()
+    rc = lib().mrt_shard_pixels(width, height, shard_index, shard_count, None, C.byref(n))
+    if rc != 0:
+        raise MassrtError(lib().mrt_global_last_error().decode())
+    out = np.empty(max(n.value, 1), dtype=np.uint32)
+    rc = lib().mrt_shard_pixels(width, height, shard_index, shard_count, out.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                C.byref(n))
+    if rc != 0:
+        raise MassrtError(lib().mrt_global_last_error().decode())
+    return out[: n.value]
 
 
 DISPLAY_DEFAULT, DISPLAY_DEPTH, DISPLAY_ALBEDO, DISPLAY_NORMAL = 0, 1, 2, 3

@@ -65,7 +65,7 @@ def lib() -> C.CDLL:
         "orc_trace_rays": (I, [P, fp, U32, F, F, P]),
         "orc_render": (I, [P, U32, U32, U32, U32, U64, U32, U32, U32, I, fp, up]),
         "orc_render_pixels": (I, [P, U32, U32, up, U32, U32, U32, U64, U32, I, fp, up]),
-        "orc_bench_reference_mode": (C.c_double, [P, U32, U32, U32, U64, U32, I, fp, up, U32, U32]),
+        "orc_bench_reference_mode": (C.c_double, [P, U32, U32, U32, U64, U32, I, fp, up, U32, U32, U32]),
         "orc_get_counters": (None, [P, P]),
         "orc_wyrand": (None, [U64, U32, C.POINTER(C.c_uint64), fp]),
         "orc_path_rng": (None, [U64, U32, U32, U32, C.POINTER(C.c_uint64), fp]),
@@ -284,11 +284,11 @@ class Scene:
         return rgb, b
 
     def bench_reference_mode(self, width, height, passes_per_thread, seed=1, max_depth=50, threads=0, row_begin=0,
-                             row_end=0):
+                             row_end=0, row_step=1):
         rgb = np.zeros(width * height * 3, dtype=np.float32)
         b = np.zeros(width * height, dtype=np.uint32)
         secs = lib().orc_bench_reference_mode(self.h, width, height, passes_per_thread, seed, max_depth, threads,
-                                              _fp(rgb), _up(b), row_begin, row_end)
+                                              _fp(rgb), _up(b), row_begin, row_end, row_step)
         if secs < 0:
             raise OracleError("reference-mode bench failed")
         return secs, rgb, b

@@ -1747,9 +1747,10 @@ int orc_render(orc_scene* s, uint32_t W, uint32_t H, uint32_t spp_begin, uint32_
 // (row-restricted) frame into its own ImageBuffer, then merges under a Mutex.
 double orc_bench_reference_mode(orc_scene* s, uint32_t W, uint32_t H, uint32_t passes, uint64_t seed,
                                 uint32_t max_depth, int threads, float* rgb, uint32_t* bo, uint32_t row_begin,
-                                uint32_t row_end) {
+                                uint32_t row_end, uint32_t row_step) {
   if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
   if (row_end > H || row_end == 0) row_end = H;
+  if (row_step == 0) row_step = 1;
   std::mutex image_mu;
   std::atomic<uint32_t> pass_counter{0};
   auto t0 = std::chrono::steady_clock::now();
@@ -1762,13 +1763,13 @@ double orc_bench_reference_mode(orc_scene* s, uint32_t W, uint32_t H, uint32_t p
       try {
         for (uint32_t k = 0; k < passes; ++k) {
           uint32_t sample = pass_counter.fetch_add(1);
-          for (uint32_t y = row_begin; y < row_end; ++y)
+          for (uint32_t y = row_begin; y < row_end; y += row_step)
             for (uint32_t x = 0; x < W; ++x) {
               uint32_t p = y * W + x;
               sample_pixel(s, W, H, p, sample, seed, max_depth, c, buffer[p].first, buffer[p].second);
             }
           std::lock_guard<std::mutex> g(image_mu);
-          for (uint32_t y = row_begin; y < row_end; ++y)
+          for (uint32_t y = row_begin; y < row_end; y += row_step)
             for (uint32_t x = 0; x < W; ++x) {
               size_t p = (size_t)y * W + x;
               rgb[3 * p] += buffer[p].first.x, rgb[3 * p + 1] += buffer[p].first.y, rgb[3 * p + 2] += buffer[p].first.z;

@@ -93,10 +93,12 @@ int orc_render_pixels(orc_scene* s, uint32_t W, uint32_t H, const uint32_t* pixe
                       uint32_t* out_b);
 // Reference-mode CPU baseline (main.rs:159-290): `threads` workers, each
 // rendering whole 1-spp frames into a private buffer merged under a mutex,
-// for `passes_per_thread` passes. Returns wall seconds (< 0 on error).
+// for `passes_per_thread` passes. Only rows row_begin, row_begin + row_step,
+// ... < row_end are rendered (a stratified sample of the frame for timing).
+// Returns wall seconds (< 0 on error).
 double orc_bench_reference_mode(orc_scene* s, uint32_t W, uint32_t H, uint32_t passes_per_thread, uint64_t seed,
                                 uint32_t max_depth, int threads, float* accum_rgb, uint32_t* accum_bounces,
-                                uint32_t row_begin, uint32_t row_end);
+                                uint32_t row_begin, uint32_t row_end, uint32_t row_step);
 void orc_wyrand(uint64_t seed, uint32_t n, uint64_t* out_u64, float* out_f32);
 void orc_path_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint64_t* out_u64, float* out_f32);
 // Image::to_rgb_bytes (main.rs:640-722) + dump's row flip (main.rs:760-767):

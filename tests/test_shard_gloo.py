@@ -1,11 +1,11 @@
 """Multi-rank sharding path (massrt/shard.py, used by bench.py --gpus N) on
-CPU ranks over gloo: each rank accumulates its 8x8 tiles, one reduce per step
+CPU ranks over gloo: each rank accumulates its 8x8 tiles, one slab gather per step
 publishes the frame on rank 0. The oracle stands in for the GPU renderer
 here (test infrastructure only); the GPU tests cover the device side of the
 same shard_index/shard_count arguments.
 
 Expected: the published frame is bit-identical to a single-rank render of
-the same samples (disjoint tiles — the reduce only adds zeros).
+the same samples (every pixel is summed on one rank only).
 """
 import os
 import socket
