@@ -12,8 +12,11 @@
 // therefore its closest hit, ties included — with no traversal stack.
 // Instances/models jump into a shared BLAS region and return (one level).
 //
-// Records are made of 16-byte slots (uint4); the kind is always slot1.w:
-//   BOX    2 slots  {min.x,min.y,min.z,max.x} {max.y,max.z,skip,BOX}
+// Records are made of 16-byte slots (uint4); the kind is slot1.w, and a box
+// says it is one by bit 31 there (kBoxFlag), the rest of that word being the
+// index its box-hit step goes to (its first child: the next record of the
+// plain stream):
+//   BOX    2 slots  {min.x,min.y,min.z,max.x} {max.y,max.z,skip,kBoxFlag|hit}
 //   SPHERE 2 slots  {cx,cy,cz,r}              {sphere_id,0,0,SPHERE}
 //   TRI    3 slots  {a.x,a.y,a.z,ab.x}        {ab.y,ab.z,tri_id,TRI} {ac.x,ac.y,ac.z,flags}
 //   INST   2 slots  {inst_id,blas_begin,blas_end,0} {0,0,0,INST}
@@ -28,6 +31,16 @@
 namespace mrt {
 
 enum : uint32_t { KIND_BOX = 1, KIND_SPHERE = 2, KIND_TRI = 3, KIND_INST = 4, KIND_MODEL = 5, KIND_VOLUME = 6 };
+constexpr uint32_t kBoxFlag = 0x80000000u;  // slot1.w of a box: kBoxFlag | hit index
+// LDS treelet (upload.cpp build_treelet): the most visited records are copied
+// into every k_trace workgroup's LDS. An index with kLdsTag names slot
+// (index & kIdxMask) of that copy; box hit/skip indices and instance/model
+// BLAS entries are rewritten to reach the copies, in the copy itself and in a
+// rewritten global stream (slots_tl) the LDS kernels read instead of slots.
+// Whole regions are copied contiguously, so a primitive's implicit "next
+// record" stays inside the copy; other primitives are never copied.
+constexpr uint32_t kLdsTag = 0x40000000u;
+constexpr uint32_t kIdxMask = 0x3FFFFFFFu;
 // the region being traversed has ended (record after its last one; path.h)
 constexpr uint32_t KIND_END = 0;
 enum : uint32_t { TRI_FLAG_ALPHA = 1u, TRI_FLAG_UV = 2u };
@@ -104,6 +117,11 @@ struct DevScene {
   float bg_color[4];
   const GpuSurfRef* bg_faces;  // SkySphere: 1 surface; CubeMap: x_pos x_neg y_pos y_neg z_pos z_neg
   const float* bg_m;           // CubeMap transform, column-major 4x4
+  // LDS treelet (n_tlet == 0: none)
+  const uint32_t* slots_tl;    // the record stream with indices rewritten to reach the treelet
+  const uint32_t* tlet;        // the treelet image copied into LDS (n_tlet slots of 4 words)
+  uint32_t n_tlet;
+  uint32_t tl_world_begin;     // world entry index beside the treelet (possibly LDS-tagged)
 };
 
 }  // namespace mrt

@@ -349,7 +349,8 @@ struct Hit {
 // closest t so far is `best` (Hit.t is filled in by trav_hit()).
 struct TravIn {
   const DevScene& S;
-  const uint4* slots;      // record stream (global, or its LDS copy)
+  const uint4* slots;      // record stream in global memory (S.slots, or S.slots_tl beside an LDS treelet)
+  uint32_t world_begin;    // first record of the world region (an LDS-tagged index beside a treelet)
   const float4* ro;        // ray origins  (xyz) of the pool
   const float4* rd;        // ray directions (xyz)
   float tmin;
@@ -376,12 +377,35 @@ struct Trav {
 #endif
 };
 
+// LDS treelet (layout.h): records with kLdsTag in their index live in the
+// workgroup's LDS copy (mrt_lds), the rest in the global stream. Kernels
+// built with LDS=false never see a tagged index.
+extern __shared__ uint4 mrt_lds[];
+template <bool LDS>
+MRT_DEV void rec_load2(const TravIn& in, uint32_t i, uint4& a, uint4& b) {
+  if (LDS && (i & kLdsTag)) {
+    const uint32_t j = i & kIdxMask;
+    a = mrt_lds[MRT_IDX(in.S, j, in.S.n_tlet, 22)];
+    b = mrt_lds[MRT_IDX(in.S, j + 1, in.S.n_tlet, 22)];
+  } else {
+    MRT_IDX(in.S, i + 1, in.S.n_slots, 6);
+    const uint4* p = in.slots + MRT_IDX(in.S, i, in.S.n_slots, 5);  // one address, offset:16 for slot 2
+    a = p[0];
+    b = p[1];
+  }
+}
+template <bool LDS>
+MRT_DEV uint4 rec_load1(const TravIn& in, uint32_t i) {
+  if (LDS && (i & kLdsTag)) return mrt_lds[MRT_IDX(in.S, i & kIdxMask, in.S.n_tlet, 22)];
+  return in.slots[MRT_IDX(in.S, i, in.S.n_slots, 7)];
+}
+
+template <bool LDS = false>
 MRT_DEV Hit trav_hit(const TravIn& in, const Trav& t) {
   uint32_t container = kRefNone;
   if (t.hit_ret != kNoRet) {
     const uint32_t rec = (t.hit_ret & ~kRetInstance) - 2;  // the instance/model record
-    container = make_ref((t.hit_ret & kRetInstance) ? MRT_REF_INSTANCE : MRT_REF_MODEL,
-                         in.slots[MRT_IDX(in.S, rec, in.S.n_slots, 11)].x);
+    container = make_ref((t.hit_ret & kRetInstance) ? MRT_REF_INSTANCE : MRT_REF_MODEL, rec_load1<LDS>(in, rec).x);
   }
   return Hit{t.best, t.prim, container};
 }
@@ -468,19 +492,16 @@ MRT_DEV TRay world_ray(const TravIn& in, uint32_t ray) {
 
 // Load record t.i. Every region ends in an END record (handled by
 // trav_prim: leave the BLAS, or finish), so there is no bounds compare here.
+template <bool LDS = false>
 MRT_DEV void trav_fetch(const TravIn& in, Trav& t) {
-  const DevScene& S = in.S;
 #ifdef MRT_DEBUG_BOUNDS
-  if (t.i + 1 >= S.n_slots || ++t.steps > (1u << 24)) {  // record and stop instead of looping/faulting
-    MRT_IDX(S, t.i + 1 >= S.n_slots ? t.i : 0xFFFFFFF0u, t.i + 1 >= S.n_slots ? S.n_slots : 0u, 5);
+  if (++t.steps > (1u << 24)) {  // record and stop instead of looping
+    MRT_IDX(in.S, 0xFFFFFFF0u, 0u, 5);
     t.done = true;
     return;
   }
 #endif
-  MRT_IDX(S, t.i + 1, S.n_slots, 6);
-  const uint4* p = in.slots + MRT_IDX(S, t.i, S.n_slots, 5);  // one address, offset:16 for slot 2
-  t.s0 = p[0];
-  t.s1 = p[1];
+  rec_load2<LDS>(in, t.i, t.s0, t.s1);
 }
 
 // The region ended: leave the BLAS back to the world ray (geom.rs:405-409;
@@ -497,7 +518,7 @@ MRT_DEV void trav_end_index(const TravIn& in, Trav& t) {
 }
 
 // Start ray `ray` of the pool (World::intersect(ray, in.tmin, tmax)).
-template <bool RNG = false>
+template <bool RNG = false, bool LDS = false>
 MRT_DEV void trav_init(const TravIn& in, Trav& t, uint32_t ray, float tmax) {
   if (RNG) {
     const uint4 q = in.rng[ray];
@@ -506,7 +527,7 @@ MRT_DEV void trav_init(const TravIn& in, Trav& t, uint32_t ray, float tmax) {
   }
   t.r = world_ray(in, ray);
   t.ray = ray;
-  t.i = in.S.world_begin;
+  t.i = in.world_begin;
   t.ret = kNoRet;
   t.best = tmax;
   t.prim = kRefNone;
@@ -515,18 +536,18 @@ MRT_DEV void trav_init(const TravIn& in, Trav& t, uint32_t ray, float tmax) {
 #ifdef MRT_DEBUG_BOUNDS
   t.steps = 0;
 #endif
-  trav_fetch(in, t);
+  trav_fetch<LDS>(in, t);
 }
 
-MRT_DEV bool trav_at_box(const Trav& t) { return t.s1.w == KIND_BOX; }
+MRT_DEV bool trav_at_box(const Trav& t) { return (int32_t)t.s1.w < 0; }  // kBoxFlag (layout.h)
 
 // The current record is a box: test it and move on.
-template <bool COUNT>
+template <bool COUNT, bool LDS = false>
 MRT_DEV void trav_box(const TravIn& in, Trav& t, LocalCounters& lc) {
   if (COUNT) lc.node_visits++;
   V3 mn{u2f(t.s0.x), u2f(t.s0.y), u2f(t.s0.z)}, mx{u2f(t.s0.w), u2f(t.s1.x), u2f(t.s1.y)};
-  t.i = box_hit_any(mn, mx, t.r, in.tmin, t.best) ? t.i + 2 : t.s1.z;
-  trav_fetch(in, t);
+  t.i = box_hit_any(mn, mx, t.r, in.tmin, t.best) ? (t.s1.w & ~kBoxFlag) : t.s1.z;
+  trav_fetch<LDS>(in, t);
 }
 
 // trav_box without the fetch of the next record (k_trace's box run loads at
@@ -539,7 +560,7 @@ MRT_DEV void trav_box_index(const TravIn& in, Trav& t, LocalCounters& lc) {
   for (int k = 0; k < MRT_PAD_VALU; ++k) asm volatile("v_nop");
 #endif
   V3 mn{u2f(t.s0.x), u2f(t.s0.y), u2f(t.s0.z)}, mx{u2f(t.s0.w), u2f(t.s1.x), u2f(t.s1.y)};
-  t.i = box_hit_any(mn, mx, t.r, in.tmin, t.best) ? t.i + 2 : t.s1.z;
+  t.i = box_hit_any(mn, mx, t.r, in.tmin, t.best) ? (t.s1.w & ~kBoxFlag) : t.s1.z;
 }
 
 // The current record is a primitive, an instance or a model. ALPHA=false is
@@ -577,7 +598,7 @@ MRT_DEV bool volume_hit(const DevScene& S, const TravIn& in, Trav& t, uint4 s0, 
 // ALPHA: 0 no alpha tests, 1 alpha tests, 2 alpha tests over EXT surfaces
 // trav_prim_index moves to the next record (or finishes the ray) without
 // loading it; trav_prim also loads it.
-template <bool COUNT, uint32_t ALPHA, bool RNG = false>
+template <bool COUNT, uint32_t ALPHA, bool RNG = false, bool LDS = false>
 MRT_DEV void trav_prim_index(const TravIn& in, Trav& t, LocalCounters& lc) {
   const DevScene& S = in.S;
   const uint4 s0 = t.s0, s1 = t.s1;
@@ -588,7 +609,7 @@ MRT_DEV void trav_prim_index(const TravIn& in, Trav& t, LocalCounters& lc) {
   }
   if (kind == KIND_TRI) {
     if (COUNT) lc.triangle_tests++;
-    const uint4 s2 = in.slots[MRT_IDX(S, t.i + 2, S.n_slots, 7)];
+    const uint4 s2 = rec_load1<LDS>(in, t.i + 2);
     V3 a{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, ab{u2f(s0.w), u2f(s1.x), u2f(s1.y)}, ac{u2f(s2.x), u2f(s2.y), u2f(s2.z)};
     float th;
     if (tri_hit(a, ab, ac, t.r.o, t.r.d, in.tmin, t.best, th)) {
@@ -630,10 +651,10 @@ MRT_DEV void trav_prim_index(const TravIn& in, Trav& t, LocalCounters& lc) {
     t.i = s0.y;
   }
 }
-template <bool COUNT, uint32_t ALPHA, bool RNG = false>
+template <bool COUNT, uint32_t ALPHA, bool RNG = false, bool LDS = false>
 MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
-  trav_prim_index<COUNT, ALPHA, RNG>(in, t, lc);
-  if (!t.done) trav_fetch(in, t);
+  trav_prim_index<COUNT, ALPHA, RNG, LDS>(in, t, lc);
+  if (!t.done) trav_fetch<LDS>(in, t);
 }
 
 // Whole traversal of pool ray `ray` (one ray per thread); RNG: the

@@ -171,30 +171,31 @@ struct TraceTune {
   uint32_t shade_batch = 16; // k_render: shade once this many lanes finished a segment
 };
 
-// LDS=true: the whole record stream is first copied into the workgroup's LDS
-// (scenes up to kTraceLdsMaxBytes, e.g. SphereGrid's ~31 KB), so every
-// traversal step reads LDS instead of L1/L2.
-constexpr size_t kTraceLdsMaxBytes = 64 * 1024;
+// LDS=true: the scene's treelet (layout.h, upload.cpp build_treelet) is first
+// copied into the workgroup's LDS; records with an LDS-tagged index are then
+// read there (ds_read_b128) instead of through L1/L2 — the top of the trees,
+// which every ray visits, and small instanced BLAS whole. BLK threads per
+// workgroup share one copy.
+constexpr size_t kTraceLdsMaxBytes = 160 * 1024;
 constexpr uint32_t kIdle = 0xFFFFFFFFu;  // Trav.ray of a lane without a ray
 
 // RNG: the scene's traversal draws random numbers (Volume, Mix alpha tests):
 // each ray carries its path stream through the traversal and stores it back.
 // (R > 1 would interleave R rays per lane — software ILP; measured slower at
 // its 84 VGPRs, so only R = 1 is instantiated.)
-template <bool COUNT, bool LDS, uint32_t ALPHA, bool RNG>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ALPHA == 0 && !RNG && !COUNT ? 8 : 1))) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
+template <bool COUNT, bool LDS, uint32_t ALPHA, bool RNG, int BLK>
+__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(ALPHA == 0 && !RNG && !COUNT ? 8 : 1))) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   DevCounters* cnt, float tmin, float tmax, TraceTune tune) {
   constexpr int R = 1;
-  extern __shared__ uint4 lds_slots[];
   const uint32_t n = ctrl->active[cur];
   if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = 0;
   if (n == 0) return;  // uniform: every workgroup reads the same n
-  const uint4* gslots = reinterpret_cast<const uint4*>(S.slots);
   if (LDS) {
-    for (uint32_t k = threadIdx.x; k < S.n_slots; k += kBlock) lds_slots[k] = gslots[k];
+    for (uint32_t k = threadIdx.x; k < S.n_tlet; k += BLK) mrt_lds[k] = reinterpret_cast<const uint4*>(S.tlet)[k];
     __syncthreads();
   }
-  const TravIn tin{S, LDS ? lds_slots : gslots, in.ro, in.rd, tmin, in.rng};
+  const TravIn tin{S, reinterpret_cast<const uint4*>(LDS ? S.slots_tl : S.slots), LDS ? S.tl_world_begin : S.world_begin,
+                   in.ro, in.rd, tmin, in.rng};
   LocalCounters lc;
   uint32_t seg = 0, nh = 0;
   uint32_t pool = 0, pool_end = 0;  // wave-uniform chunk [pool, pool_end)
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ALPHA ==
       for (int q = 0; q < R; ++q) {
         if (t[q].ray == kIdle) {
           const uint32_t r = off + lane_rank(idle[q]);
-          if (r < avail) trav_init<RNG>(tin, t[q], MRT_IDX(S, pool + r, n, 20), tmax);
+          if (r < avail) trav_init<RNG, LDS>(tin, t[q], MRT_IDX(S, pool + r, n, 20), tmax);
         }
         off += (uint32_t)__popcll(idle[q]);
         live |= __ballot(t[q].ray != kIdle);
@@ -265,9 +266,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ALPHA ==
           if (trav_at_box(t[q]))
             trav_box_index<COUNT>(tin, t[q], lc);
           else
-            trav_prim_index<COUNT, ALPHA, RNG>(tin, t[q], lc);
+            trav_prim_index<COUNT, ALPHA, RNG, LDS>(tin, t[q], lc);
         }
-        if (!t[q].done) trav_fetch(tin, t[q]);
+        if (!t[q].done) trav_fetch<LDS>(tin, t[q]);
         if (COUNT) {
           lc.wave_slots += lane_id() == 0 ? 64u : 0u;
           lc.lane_steps += busy ? 1u : 0u;
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ALPHA ==
         const unsigned long long bm = __builtin_amdgcn_ballot_w64(at_box);
         if ((uint32_t)__popcll(bm) < tune.box_min) break;
         if (at_box) trav_box_index<COUNT>(tin, t[q], lc);
-        if (at_box) trav_fetch(tin, t[q]);
+        if (at_box) trav_fetch<LDS>(tin, t[q]);
 #ifdef MRT_PROBE  // experiment builds: texel_taps = box-run iterations, wave_slots = uniform ones
         if (COUNT) {
           const uint32_t f = __builtin_amdgcn_readfirstlane(at_box ? t[q].i : 0xFFFFFFFFu);
@@ -305,10 +306,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ALPHA ==
       const bool at_box = busy && trav_at_box(t[q]);
       const unsigned long long box_mask = __ballot(at_box);
       const unsigned long long prim_mask = __ballot(busy && !at_box);
-      if (at_box) trav_box<COUNT>(tin, t[q], lc);
+      if (at_box) trav_box<COUNT, LDS>(tin, t[q], lc);
       // primitives wait until enough lanes are at one (or no lane is at a box)
       const bool prim_go = (__popcll(prim_mask) >= tune.prim_batch || box_mask == 0) && busy && !at_box;
-      if (prim_go) trav_prim<COUNT, ALPHA, RNG>(tin, t[q], lc);
+      if (prim_go) trav_prim<COUNT, ALPHA, RNG, LDS>(tin, t[q], lc);
 #ifdef MRT_PROBE
       if (COUNT) lc.model_entries += lane_id() == 0 ? 1u : 0u;  // outer iterations
 #endif
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ALPHA ==
     for (int q = 0; q < R; ++q) {
       if (t[q].ray != kIdle && t[q].done) {
         if (RNG) trav_store_rng(tin, t[q]);
-        const Hit h = trav_hit(tin, t[q]);
+        const Hit h = trav_hit<LDS>(tin, t[q]);
         hits[t[q].ray] = make_uint4(__float_as_uint(h.t), h.prim, h.container, 0u);
         seg += 1;
         nh += t[q].prim != kRefNone;
@@ -344,7 +345,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_simple(DevScene S, PathBufs in
   if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = 0;
   LocalCounters lc;
   uint32_t seg = 0, nh = 0;
-  const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), in.ro, in.rd, kTmin, in.rng};
+  const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), S.world_begin, in.ro, in.rd, kTmin, in.rng};
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     PathRng rng{0, 0};
     if (RNG) {
@@ -468,18 +469,12 @@ __global__ __launch_bounds__(kBlock, MRT_SHADE_WPE) void k_shade(DevScene S, Dev
 // idle lanes take new work items from ctrl->next_work. slot_ro/slot_rd hold
 // each lane's current world ray (re-read when leaving an instance and when
 // shading, instead of keeping it in registers).
-template <bool COUNT, bool LDS, bool ALPHA>
+template <bool COUNT, bool ALPHA>
 __global__ __launch_bounds__(kBlock) void k_render(DevScene S, DevCamera cam, RenderParams rp, float4* slot_ro,
                                                    float4* slot_rd, Ctrl* ctrl, float4* results, DevCounters* cnt,
                                                    TraceTune tune) {
-  extern __shared__ uint4 lds_slots[];
-  const uint4* gslots = reinterpret_cast<const uint4*>(S.slots);
-  if (LDS) {
-    for (uint32_t q = threadIdx.x; q < S.n_slots; q += kBlock) lds_slots[q] = gslots[q];
-    __syncthreads();
-  }
   const uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
-  const TravIn tin{S, LDS ? lds_slots : gslots, slot_ro, slot_rd, kTmin};
+  const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), S.world_begin, slot_ro, slot_rd, kTmin};
   LocalCounters lc;
   uint32_t seg = 0, nh = 0, nsamples = 0, nbounces = 0;
   Trav t{};
@@ -726,7 +721,7 @@ __global__ __launch_bounds__(kBlock) void k_prepass(DevScene S, DevCamera cam, u
   camera_ray_uv(cam, (float)x / (float)(W - 1), (float)y / (float)(H - 1), rng, o, d);
   ray_ro[p] = make_float4(o.x, o.y, o.z, 0.0f);
   ray_rd[p] = make_float4(d.x, d.y, d.z, 0.0f);
-  const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), ray_ro, ray_rd, kTmin};
+  const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), S.world_begin, ray_ro, ray_rd, kTmin};
   LocalCounters lc;
   const Hit h = closest_hit<false, RNG, EXT>(tin, p, INFINITY, lc, rng);
   V3 a{0.0f, 0.0f, 0.0f}, n{0.0f, 0.0f, 0.0f};
@@ -907,7 +902,14 @@ struct mrt_ctx {
   // hold 11 GiB of HBM (176 B each).
   size_t pool_paths = (size_t)128 << 20;
   int cus = 1;
-  bool trace_lds = false;          // record stream staged in LDS (set per scene)
+  bool trace_lds = false;          // the scene has an LDS treelet (set per scene)
+  uint32_t tl_boxes = 0;           // box records in the treelet
+  // LDS treelet: off by default. Measured: it removes the
+  // global load of a step only when every lane of the wave is in the copy,
+  // and the TA cost is per wave instruction, not per lane — 256/16 KB and
+  // 1024/78 KB were 1% and 1-4% slower than no treelet.
+  int trace_block = 256;           // k_trace workgroup size with a treelet (MRT_TRACE_BLOCK: 256 or 1024)
+  uint32_t treelet_kb = 0;         // treelet budget per workgroup (MRT_TREELET_KB; 0 = none)
 
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t*, uint32_t>> pixlists;
   // host-buffer render staging
@@ -976,13 +978,13 @@ void wait_queues(mrt_ctx* c, hipStream_t st) {
 // and shade launches find room on every CU instead of queueing behind a
 // grid that holds the whole GPU until its last ray (sphere_grid, 2 queues:
 // 8 WGs/CU 585, 6 WGs/CU 618 Msamples/s).
-uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem, bool shared = false) {
+uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem, bool shared = false, int block = kBlock) {
   auto key = std::make_pair(f, smem);
   auto it = c->grids.find(key);
   if (it != c->grids.end()) return it->second;
   if (smem > 0) HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTraceLdsMaxBytes));
   int per_cu = 0;
-  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, smem));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, smem));
   if (shared) per_cu = std::max(1, per_cu * 3 / 4);
   if (const char* e = getenv("MRT_TRACE_WGS_PER_CU")) per_cu = atoi(e);
   const uint32_t g = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
@@ -990,18 +992,29 @@ uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem, bool shared = f
   return g;
 }
 
+template <bool LDS, uint32_t ALPHA, bool RNG, int BLK>
+void launch_trace_b(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
+                    float tmin, float tmax) {
+  const size_t smem = LDS ? (size_t)c->S.n_tlet * 16 : 0;
+  const void* f = count ? (const void*)k_trace<true, LDS, ALPHA, RNG, BLK> : (const void*)k_trace<false, LDS, ALPHA, RNG, BLK>;
+  const uint32_t grid = persistent_grid(c, f, smem, c->n_queues > 1, BLK);
+  if (count)
+    hipLaunchKernelGGL((k_trace<true, LDS, ALPHA, RNG, BLK>), dim3(grid), dim3(BLK), smem, st, c->S, in, q.hits,
+                       q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
+  else
+    hipLaunchKernelGGL((k_trace<false, LDS, ALPHA, RNG, BLK>), dim3(grid), dim3(BLK), smem, st, c->S, in, q.hits,
+                       q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
+}
+
 template <bool LDS, uint32_t ALPHA, bool RNG>
 void launch_trace_r(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
                     float tmin, float tmax) {
-  const size_t smem = LDS ? (size_t)c->S.n_slots * 16 : 0;
-  const void* f = count ? (const void*)k_trace<true, LDS, ALPHA, RNG> : (const void*)k_trace<false, LDS, ALPHA, RNG>;
-  const uint32_t grid = persistent_grid(c, f, smem, c->n_queues > 1);
-  if (count)
-    hipLaunchKernelGGL((k_trace<true, LDS, ALPHA, RNG>), dim3(grid), dim3(kBlock), smem, st, c->S, in, q.hits,
-                       q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
+  if (!LDS)
+    launch_trace_b<false, ALPHA, RNG, kBlock>(c, st, q, in, cur, count, tmin, tmax);
+  else if (c->trace_block == 1024)
+    launch_trace_b<true, ALPHA, RNG, 1024>(c, st, q, in, cur, count, tmin, tmax);
   else
-    hipLaunchKernelGGL((k_trace<false, LDS, ALPHA, RNG>), dim3(grid), dim3(kBlock), smem, st, c->S, in, q.hits,
-                       q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
+    launch_trace_b<true, ALPHA, RNG, kBlock>(c, st, q, in, cur, count, tmin, tmax);
 }
 
 template <bool LDS, uint32_t ALPHA>
@@ -1115,18 +1128,17 @@ std::pair<uint32_t*, uint32_t> pixlist(mrt_ctx* c, uint32_t W, uint32_t H, uint3
 }
 
 
-template <bool LDS, bool ALPHA>
+template <bool ALPHA>
 void launch_render_v(mrt_ctx* c, hipStream_t st, const RenderParams& rp, bool count) {
-  const size_t smem = LDS ? (size_t)c->S.n_slots * 16 : 0;
-  const void* f = count ? (const void*)k_render<true, LDS, ALPHA> : (const void*)k_render<false, LDS, ALPHA>;
-  const uint32_t grid = persistent_grid(c, f, smem);
+  const void* f = count ? (const void*)k_render<true, ALPHA> : (const void*)k_render<false, ALPHA>;
+  const uint32_t grid = persistent_grid(c, f, 0);
   ensure_slots(c, (size_t)grid * kBlock);
   if (count)
-    hipLaunchKernelGGL((k_render<true, LDS, ALPHA>), dim3(grid), dim3(kBlock), smem, st, c->S, c->cam, rp, c->slot_ro,
+    hipLaunchKernelGGL((k_render<true, ALPHA>), dim3(grid), dim3(kBlock), 0, st, c->S, c->cam, rp, c->slot_ro,
                        c->slot_rd, c->q[0].ctrl, c->results, c->d_cnt, c->tune);
   else
-    hipLaunchKernelGGL((k_render<false, LDS, ALPHA>), dim3(grid), dim3(kBlock), smem, st, c->S, c->cam, rp,
-                       c->slot_ro, c->slot_rd, c->q[0].ctrl, c->results, c->d_cnt, c->tune);
+    hipLaunchKernelGGL((k_render<false, ALPHA>), dim3(grid), dim3(kBlock), 0, st, c->S, c->cam, rp, c->slot_ro,
+                       c->slot_rd, c->q[0].ctrl, c->results, c->d_cnt, c->tune);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1153,17 +1165,10 @@ void render_fused(mrt_ctx* c, const mrt_render_args* a, const uint32_t* pixlist_
     Ctrl init{{0, 0}, 0, 0};
     HIP_CHECK(hipMemcpyAsync(c->q[0].ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, st));
     if (timing) HIP_CHECK(hipEventRecord(c->tev[0], st));
-    if (c->trace_lds) {
-      if (c->scene_alpha)
-        launch_render_v<true, true>(c, st, rp, count);
-      else
-        launch_render_v<true, false>(c, st, rp, count);
-    } else {
-      if (c->scene_alpha)
-        launch_render_v<false, true>(c, st, rp, count);
-      else
-        launch_render_v<false, false>(c, st, rp, count);
-    }
+    if (c->scene_alpha)
+      launch_render_v<true>(c, st, rp, count);
+    else
+      launch_render_v<false>(c, st, rp, count);
     if (timing) {
       HIP_CHECK(hipEventRecord(c->tev[1], st));
       HIP_CHECK(hipEventSynchronize(c->tev[1]));
@@ -1397,6 +1402,11 @@ int mrt_create(int device, mrt_ctx** out) {
     if (const char* e = getenv("MRT_TRACE_BOX_MIN")) c->tune.box_min = (uint32_t)std::max(1, std::min(65, atoi(e)));
     if (const char* e = getenv("MRT_SHADE_BATCH")) c->tune.shade_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_POOL_PATHS")) c->pool_paths = (size_t)std::max(1 << 16, std::min(1 << 28, atoi(e)));
+    if (const char* e = getenv("MRT_TRACE_BLOCK")) {
+      const int b = atoi(e);
+      c->trace_block = b >= 1024 ? 1024 : 256;
+    }
+    if (const char* e = getenv("MRT_TREELET_KB")) c->treelet_kb = (uint32_t)std::max(0, std::min(150, atoi(e)));
   });
   if (rc != MRT_OK) {
     g_last_error = c->err;
@@ -1455,6 +1465,7 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     HostScene hs;
     std::string err;
     if (!build_host_scene(*d, hs, err)) throw ApiError{MRT_ERR_INVALID, err};
+    build_treelet(hs, (uint32_t)((size_t)c->treelet_kb * 1024 / 16));
     // one allocation, 256-B aligned sections
     size_t off = 0;
     auto sec = [&](size_t bytes) {
@@ -1462,7 +1473,8 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
       off += (bytes + 255) & ~(size_t)255;
       return o;
     };
-    size_t o_slots = sec(hs.slots.size() * 4), o_inv = sec(hs.inst_inv.size() * 4),
+    size_t o_slots = sec(hs.slots.size() * 4), o_stl = sec(hs.slots_tl.size() * 4), o_tlet = sec(hs.tlet.size() * 4),
+           o_inv = sec(hs.inst_inv.size() * 4),
            o_fwd = sec(hs.inst_fwd.size() * 4), o_imat = sec(hs.inst_mat.size() * 4),
            o_mmat = sec(hs.model_mat.size() * 4), o_sph = sec(hs.sph.size() * 4), o_smat = sec(hs.sph_mat.size() * 4),
            o_tri = sec(hs.tri_shade.size() * 4), o_mat = sec(hs.materials.size() * sizeof(GpuMaterial)),
@@ -1482,6 +1494,8 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
       if (bytes) HIP_CHECK(hipMemcpy(base + o, src, bytes, hipMemcpyHostToDevice));
     };
     up(o_slots, hs.slots.data(), hs.slots.size() * 4);
+    up(o_stl, hs.slots_tl.data(), hs.slots_tl.size() * 4);
+    up(o_tlet, hs.tlet.data(), hs.tlet.size() * 4);
     up(o_vnid, hs.vol_nid.data(), hs.vol_nid.size() * 4);
     up(o_vmat, hs.vol_mat.data(), hs.vol_mat.size() * 4);
     up(o_ln, ln_table.data(), ln_table.size() * 4);
@@ -1500,6 +1514,10 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     up(o_bgm, hs.bg_m, sizeof(hs.bg_m));
     DevScene S{};
     S.slots = (const uint32_t*)(base + o_slots);
+    S.slots_tl = (const uint32_t*)(base + o_stl);
+    S.tlet = (const uint32_t*)(base + o_tlet);
+    S.n_tlet = (uint32_t)(hs.tlet.size() / 4);
+    S.tl_world_begin = hs.tl_world_begin;
     S.world_begin = hs.world_begin;
     S.world_end = hs.world_end;
     S.inst_inv = (const float*)(base + o_inv);
@@ -1534,9 +1552,8 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     S.bg_m = (const float*)(base + o_bgm);
     c->S = S;
     c->scene_bytes = off;
-    const size_t lds_bytes = (size_t)S.n_slots * 16;
-    const char* no_lds = getenv("MRT_TRACE_LDS");
-    c->trace_lds = lds_bytes <= kTraceLdsMaxBytes && !(no_lds && no_lds[0] == '0');
+    c->trace_lds = S.n_tlet > 0;
+    c->tl_boxes = hs.tl_boxes;
     c->scene_alpha = hs.has_alpha;
     c->scene_rng = hs.trav_rng;
     c->scene_ext = !hs.surf_ops.empty() || hs.bg_kind == MRT_BG_CUBEMAP;

@@ -4,6 +4,9 @@
 #include <math.h>
 #include <string.h>
 
+#include <algorithm>
+#include <queue>
+#include <stdexcept>
 #include <unordered_map>
 
 namespace mrt {
@@ -270,7 +273,7 @@ struct Emitter {
         }
       }
       uint32_t at = push_slot(fbits(n.min[0]), fbits(n.min[1]), fbits(n.min[2]), fbits(n.max[0]));
-      push_slot(fbits(n.max[1]), fbits(n.max[2]), 0, KIND_BOX);
+      push_slot(fbits(n.max[1]), fbits(n.max[2]), 0, kBoxFlag | (at + 2));  // hit: the first child, next
       s.n_box_records++;
       stack.push_back({0, at});  // closes after both children
       if (MRT_REF_KIND(n.right) != MRT_REF_NONE) stack.push_back({n.right, ~0u});
@@ -401,21 +404,134 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
   s.world_end = e.n_slots();
   e.push_end();
   // BLAS regions, one per distinct root, emitted once and shared
-  std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> blas;
+  std::unordered_map<uint32_t, size_t> blas;  // BLAS root node -> s.blas_regions index
   for (auto& p : e.jump_patches) {
     auto it = blas.find(p.second);
     if (it == blas.end()) {
       uint32_t b = e.n_slots();
       if (!e.emit_tree(MRT_REF(MRT_REF_NODE, p.second), true)) return false;
-      it = blas.emplace(p.second, std::make_pair(b, e.n_slots())).first;
+      s.blas_regions.push_back({b, e.n_slots(), 0, false});
+      it = blas.emplace(p.second, s.blas_regions.size() - 1).first;
       e.push_end();
     }
-    s.slots[4 * p.first + 1] = it->second.first;
-    s.slots[4 * p.first + 2] = it->second.second;
+    BlasRegion& r = s.blas_regions[it->second];
+    r.refs++;
+    if (s.slots[4 * (p.first + 1) + 3] == KIND_MODEL) r.model = true;
+    s.slots[4 * p.first + 1] = r.begin;
+    s.slots[4 * p.first + 2] = r.end;
   }
   if (e.mix_alpha) s.trav_rng = true;
-  if (s.slots.size() / 4 >= 0x80000000ull) return (err = "scene too large (record stream >= 2^31 slots)", false);
+  if (s.slots.size() / 4 >= kLdsTag) return (err = "scene too large (record stream >= 2^30 slots)", false);
   return true;
+}
+
+// ---- LDS treelet -----------------------------------------------------------
+
+namespace {
+
+uint32_t rec_slots(const std::vector<uint32_t>& w, uint32_t i) {
+  const uint32_t k = w[4 * (i + 1) + 3];
+  return (k & kBoxFlag) ? 2 : (k == KIND_TRI ? 3 : 2);
+}
+bool rec_is_box(const std::vector<uint32_t>& w, uint32_t i) { return (w[4 * (i + 1) + 3] & kBoxFlag) != 0; }
+double box_area(const std::vector<uint32_t>& w, uint32_t i) {
+  float v[6];
+  memcpy(v, &w[4 * i], 16);
+  memcpy(v + 4, &w[4 * (i + 1)], 8);
+  const double dx = (double)v[3] - v[0], dy = (double)v[4] - v[1], dz = (double)v[5] - v[2];
+  const double a = 2.0 * (dx * dy + dy * dz + dz * dx);
+  return a == a ? a : 1e300;  // NaN/inf boxes: treat as always visited
+}
+
+}  // namespace
+
+void build_treelet(HostScene& s, uint32_t budget) {
+  const std::vector<uint32_t>& w = s.slots;
+  const uint32_t n = (uint32_t)(w.size() / 4);
+  s.tlet.clear();
+  s.slots_tl.clear();
+  s.tl_world_begin = s.world_begin;
+  s.tl_boxes = 0;
+  if (budget < 2 || n == 0) return;
+  std::vector<uint8_t> staged(n, 0);  // record starts chosen for the LDS copy
+  uint32_t used = 0;
+  auto stage_range = [&](uint32_t b, uint32_t e) {  // every record of [b, e)
+    for (uint32_t i = b; i < e; i += rec_slots(w, i)) staged[i] = 1;
+    used += e - b;
+  };
+  if (n <= budget) {
+    stage_range(0, n);  // small scene: the whole stream
+  } else {
+    // 1. small BLAS regions whole (each instance/model entry then runs in LDS),
+    //    the most referenced first, within a quarter of the budget
+    std::vector<size_t> order(s.blas_regions.size());
+    for (size_t k = 0; k < order.size(); ++k) order[k] = k;
+    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+      const BlasRegion &x = s.blas_regions[a], &y = s.blas_regions[b];
+      return x.refs != y.refs ? x.refs > y.refs : (x.end - x.begin) < (y.end - y.begin);
+    });
+    std::vector<uint8_t> whole(s.blas_regions.size(), 0);
+    for (size_t k : order) {
+      const BlasRegion& r = s.blas_regions[k];
+      const uint32_t size = r.end + 2 - r.begin;  // + its END record
+      if (size <= budget / 8 && used + size <= budget / 4) {
+        stage_range(r.begin, r.end + 2);
+        whole[k] = 1;
+      }
+    }
+    // 2. boxes by surface area (the probability that a ray meets them), from
+    //    the world roots and the roots of model BLAS (same space): a child's
+    //    area never exceeds its parent's, so the chosen set is a rooted treelet
+    std::priority_queue<std::pair<double, uint32_t>> pq;
+    auto push_children = [&](uint32_t i) {
+      for (uint32_t j = i + 2, end = w[4 * (i + 1) + 2]; j < end;
+           j = rec_is_box(w, j) ? w[4 * (j + 1) + 2] : j + rec_slots(w, j))
+        if (rec_is_box(w, j) && !staged[j]) pq.push({box_area(w, j), j});
+    };
+    for (uint32_t j = s.world_begin; j < n && w[4 * (j + 1) + 3] != KIND_END;
+         j = rec_is_box(w, j) ? w[4 * (j + 1) + 2] : j + rec_slots(w, j))
+      if (rec_is_box(w, j)) pq.push({box_area(w, j), j});
+    for (size_t k = 0; k < s.blas_regions.size(); ++k)
+      if (!whole[k] && s.blas_regions[k].model && rec_is_box(w, s.blas_regions[k].begin))
+        pq.push({box_area(w, s.blas_regions[k].begin), s.blas_regions[k].begin});
+    while (!pq.empty() && used + 2 <= budget) {
+      const uint32_t i = pq.top().second;
+      pq.pop();
+      staged[i] = 1;
+      used += 2;
+      push_children(i);
+    }
+  }
+  // LDS image: the chosen records in stream order (whole regions stay contiguous)
+  std::vector<uint32_t> lds_at(n, ~0u);
+  for (uint32_t i = 0, at = 0; i < n; i += rec_slots(w, i))
+    if (staged[i]) {
+      lds_at[i] = at;
+      at += rec_slots(w, i);
+      if (rec_is_box(w, i)) s.tl_boxes++;
+      const uint32_t nx = i + rec_slots(w, i);
+      if (!rec_is_box(w, i) && w[4 * (i + 1) + 3] != KIND_END && !(nx < n && staged[nx]))
+        throw std::logic_error("treelet: a copied primitive's next record is not copied");
+    }
+  auto R = [&](uint32_t g) { return g < n && lds_at[g] != ~0u ? (kLdsTag | lds_at[g]) : g; };
+  auto rewrite = [&](uint32_t* rec) {  // rec: 8 words of one record's first two slots
+    if (rec[7] & kBoxFlag) {
+      rec[6] = R(rec[6]);
+      rec[7] = kBoxFlag | R(rec[7] & ~kBoxFlag);
+    } else if (rec[7] == KIND_INST || rec[7] == KIND_MODEL) {
+      rec[1] = R(rec[1]);
+    }
+  };
+  s.slots_tl = w;
+  for (uint32_t i = 0; i < n; i += rec_slots(w, i)) {
+    rewrite(&s.slots_tl[4 * i]);
+    if (staged[i]) {
+      const size_t at = s.tlet.size();
+      s.tlet.insert(s.tlet.end(), w.begin() + 4 * (size_t)i, w.begin() + 4 * (size_t)(i + rec_slots(w, i)));
+      rewrite(&s.tlet[at]);
+    }
+  }
+  s.tl_world_begin = R(s.world_begin);
 }
 
 }  // namespace mrt

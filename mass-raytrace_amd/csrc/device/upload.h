@@ -8,6 +8,12 @@
 
 namespace mrt {
 
+// A BLAS region of the stream: records [begin, end) plus the END record at end.
+struct BlasRegion {
+  uint32_t begin, end, refs;  // refs: instance/model records entering it
+  bool model;                 // entered by a model (world space) at least once
+};
+
 struct HostScene {
   std::vector<uint32_t> slots;  // 4 words per slot
   uint32_t world_begin = 0, world_end = 0;
@@ -34,11 +40,23 @@ struct HostScene {
   float bg_color[4] = {0, 0, 0, 0};
   std::vector<GpuSurfRef> bg_faces;  // SkySphere 1, CubeMap 6
   float bg_m[16] = {0};
+  std::vector<BlasRegion> blas_regions;
+  // LDS treelet (build_treelet): image (4 words per slot), rewritten stream, world entry
+  std::vector<uint32_t> tlet, slots_tl;
+  uint32_t tl_world_begin = 0, tl_boxes = 0;
   // statistics
   uint32_t n_box_records = 0, n_prim_records = 0, max_depth = 0;
 };
 
 // Validates the description and linearises it. Returns false with `err` set.
 bool build_host_scene(const mrt_scene_desc& d, HostScene& out, std::string& err);
+
+// Chooses the records copied into LDS by every k_trace workgroup (at most
+// `budget` 16-byte slots): the whole stream when it fits; else the small BLAS
+// regions whole (most referenced first, within budget/4) and then boxes of the
+// world tree and of model BLAS in decreasing surface area — a rooted treelet.
+// Fills s.tlet (the LDS image), s.slots_tl (the stream with its indices
+// rewritten to reach the copies) and s.tl_world_begin. budget 0: no treelet.
+void build_treelet(HostScene& s, uint32_t budget);
 
 }  // namespace mrt

@@ -552,3 +552,33 @@ def test_menger_parity(ctx, assets_dir, scene):
         assert np.array_equal(bo[px], obo)
         assert rel_l2(rgb.reshape(-1, 3)[px], orgb.reshape(-1, 3)) <= RTOL
         assert bo.mean() / spp > 1.0  # the sponge and the ground are in view
+
+
+@pytest.mark.parametrize("block,kb", [(256, 0), (256, 1), (256, 4), (256, 24), (1024, 78), (1024, 150)])
+def test_treelet_budgets_bit_exact(golden_dir, monkeypatch, block, kb):
+    """The LDS treelet (upload.cpp build_treelet) at several budgets and
+    workgroup sizes: no treelet, a few boxes, the top of the trees, small
+    BLAS regions whole, whole small scenes. Closest hits and traversal
+    counters must equal the oracle's for every choice of copied records."""
+    monkeypatch.setenv("MRT_TRACE_BLOCK", str(block))
+    monkeypatch.setenv("MRT_TREELET_KB", str(kb))
+    c = massrt.Context(0)
+    try:
+        for scene in SMALL:
+            b = massrt.Builder(1).builtin(scene, ASPECT, golden_dir)
+            o = oracle.Scene(1).builtin(scene, ASPECT, golden_dir)
+            c.upload(b)
+            _, cam = b.desc()
+            for rays in (random_rays(3000, 11), camera_rays(cam, 3000, 12)):
+                assert np.array_equal(c.trace_rays(rays), o.trace_rays(rays)), (scene, block, kb)
+            c.reset_counters()
+            o.reset_counters()
+            rgb, bo = c.render(40, 23, 0, 2, seed=4, counters=True)
+            orgb, obo = o.render(40, 23, 0, 2, seed=4)
+            assert np.array_equal(bo, obo), (scene, block, kb)
+            assert rel_l2(rgb, orgb) <= RTOL
+            gc, oc = c.counters(), o.counters()
+            for k in massrt.COUNTER_FIELDS:
+                assert gc[k] == oc[k], (scene, block, kb, k, gc[k], oc[k])
+    finally:
+        c.close()

@@ -101,3 +101,26 @@ def test_shard_pack_unpack_roundtrip(ctx):
         assert torch.equal(s[:, :3], rgb.view(-1, 3).cpu()[pt])
         assert torch.equal(s[:, 3].contiguous().view(torch.int32), bo.cpu()[pt])
     assert torch.equal(out_rgb, rgb) and torch.equal(out_b, bo)
+
+
+def test_cpp_multi_device_driver_matches_one_device(ctx, golden_dir, tmp_path):
+    """examples/mrt_render_multi.cpp (one process, one context per device,
+    slabs gathered with peer copies) on devices 0,0,0 — three shards on the
+    one GPU here — writes the one-device image: raw sums bit-exact. (Its RCCL
+    transport needs distinct devices and is not exercised on a 1-GPU box.)"""
+    import subprocess
+
+    import massrt
+
+    exe = Path(massrt.__file__).parent / "mrt_render_multi"
+    Wc, Hc, passes = 100, 57, 3
+    raw = tmp_path / "frame.raw"
+    r = subprocess.run([str(exe), "cube_field", str(Wc), str(Hc), str(passes), str(tmp_path / "m.png"),
+                        str(golden_dir), "0,0,0", "peer", str(raw)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    b = massrt.Builder(1).builtin("cube_field", float(massrt.ASPECT_RATIO), golden_dir)
+    ctx.upload(b)
+    rgb, bo = ctx.render(Wc, Hc, 0, passes, seed=1)
+    data = np.fromfile(raw, dtype=np.uint32)
+    assert np.array_equal(data[: Wc * Hc * 3], rgb.view(np.uint32))
+    assert np.array_equal(data[Wc * Hc * 3:], bo)
