@@ -205,6 +205,37 @@ def cpu_baseline(scene: str, W: int, H: int, max_depth: int, seconds: float, see
     return out
 
 
+def c1_runs(a) -> dict:
+    """BASELINE config 1: SphereGrid (the reference's random-spheres scene,
+    sphere_grid.rs:23-94) at 400x225x64 spp, whole frame — the reference-mode
+    CPU run (min(num_cpus-2, 64) workers x whole 1-spp passes = 64 passes,
+    main.rs:159-290) and the same 64 spp on the GPU."""
+    import torch
+
+    import massrt
+    import oracle
+
+    W, H, spp = 400, 225, 64
+    threads = max(1, min((os.cpu_count() or 1) - 2, spp))
+    o = oracle.Scene(1).builtin("sphere_grid", float(massrt.ASPECT_RATIO), str(REPO / "tests" / "golden"))
+    secs, _, _ = o.bench_reference_mode(W, H, spp // threads, seed=a.seed, max_depth=a.max_depth, threads=threads)
+    cpu_samples = W * H * threads * (spp // threads)
+    ctx = massrt.Context(torch.cuda.current_device())
+    b = massrt.Builder(1).builtin("sphere_grid", float(massrt.ASPECT_RATIO), str(REPO / "tests" / "golden"))
+    ctx.upload(b)
+    b.close()
+    ctx.render(W, H, 0, 4, seed=a.seed)  # warm up
+    t0 = time.perf_counter()
+    ctx.render(W, H, 0, spp, seed=a.seed)  # host buffers in and out (the whole mrt_render call)
+    gsecs = time.perf_counter() - t0
+    ctx.close()
+    return {"workload": f"sphere_grid {W}x{H}x{spp}spp (BASELINE config 1)",
+            "cpu": {"value": round(cpu_samples / secs / 1e6, 4), "unit": "Msamples/s", "seconds": round(secs, 2),
+                    "threads": threads, "passes_per_thread": spp // threads, "kind": "port"},
+            "gpu": {"value": round(W * H * spp / gsecs / 1e6, 2), "unit": "Msamples/s", "seconds": round(gsecs, 4),
+                    "note": "one mrt_render call incl. host copies; too small to fill the GPU"}}
+
+
 def load_pmc(path: Path, stamp: dict):
     """PMC summary for this exact configuration and source, else None."""
     if not path.exists():
@@ -367,6 +398,13 @@ def main():
     if a.secondary and a.secondary != "none" and a.secondary != a.scene:
         sec = run_scene(a, a.secondary, a.secondary_steps, 1, rank, world, dev, cpu)
 
+    c1 = None
+    if cpu:
+        try:
+            c1 = c1_runs(a)
+        except Exception as e:
+            c1 = {"error": str(e)}
+
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -397,6 +435,8 @@ def main():
         for k in ("gpu_over_cpu", "gpu_over_cpu_host_estimate"):
             if k in head:
                 line["config"][k] = head[k]
+        if c1:
+            line["config"]["c1"] = c1
         if sec:
             sec["workload"] = f"{sec['scene']} {a.width}x{a.height}x{a.total_spp}spp, max_depth {a.max_depth} " \
                               f"(north_star target: 1M-triangle binary PLY, BASELINE config 4)"

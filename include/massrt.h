@@ -377,7 +377,8 @@ int mrt_builder_build_bvh(mrt_builder* b); /* World::build_bvh (world.rs:117-122
 /* World::build_bvh with the top-level tree built on ctx's device
  * (csrc/device/build.hip): the same nodes, node numbering
  * and scene-stream draws as mrt_builder_build_bvh (BvhNode::new,
- * geom.rs:110-161). MRT_ERR_INVALID for a NaN sort key. */
+ * geom.rs:110-161). MRT_ERR_INVALID for a NaN sort key in a node of >= 3 items;
+ * a failed build leaves the world and the scene stream unchanged. */
 int mrt_builder_build_bvh_device(mrt_builder* b, mrt_ctx* ctx);
 /* mrt_builder_builtin with the scene's World::build_bvh done on ctx's device */
 int mrt_builder_builtin_device(mrt_builder* b, const char* name, float aspect_ratio, const char* asset_dir,

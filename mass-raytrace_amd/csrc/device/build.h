@@ -27,7 +27,8 @@ struct DeviceBuildStats {
 
 // Appends the tree over `items` to `nodes` (preorder numbering from
 // nodes.size()); `rng` advances exactly as World::bvh_new's calls would.
-// Throws Error on an empty list or a NaN sort key (the reference's sort
+// Throws Error on an empty list or a NaN sort key in a node of 3 or more
+// items (2-item nodes compare once, as the host builder does; the reference's sort
 // comparator is not a strict weak order over NaN).
 void device_build_tree(int device, const std::vector<Item>& items, mrt::WyRand& rng, std::vector<mrt_node>& nodes,
                        BoundingBox& root_box, DeviceBuildStats* stats = nullptr);

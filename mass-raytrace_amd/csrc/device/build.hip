@@ -61,8 +61,17 @@ __global__ __launch_bounds__(kBuildBlock) void k_level_keys(const Seg* segs, uin
     const Seg s = segs[a - 1];
     if (i < s.lo + s.cnt) {
       const float f = bmin[(size_t)s.axis * n + perm[i]];
-      if (f != f) atomicOr(nan_flag, 1u);
-      key = ((unsigned long long)s.lo << 32) | order_key(f);
+      uint32_t k = order_key(f);
+      if (s.cnt == 2) {
+        // 2 items: the reference compares once, `a < b` with a = the last
+        // item (geom.rs:123-129); a NaN makes it false, so the first item
+        // goes left — equal keys keep that order in the stable sort
+        const float g = bmin[(size_t)s.axis * n + perm[i == s.lo ? i + 1 : s.lo]];
+        if (f != f || g != g) k = 0;
+      } else if (f != f) {
+        atomicOr(nan_flag, 1u);  // >= 3 items: no order over NaN keys
+      }
+      key = ((unsigned long long)s.lo << 32) | k;
     }
   }
   keys[i] = key;

@@ -353,11 +353,16 @@ void World::build_bvh(const TreeBuilder& builder) {
   std::vector<Item> items = std::move(objects_);
   objects_.clear();
   const uint32_t root = (uint32_t)nodes_.size();
+  const mrt::WyRand saved_rng = rng;  // the builder draws every axis before its device work can fail
   BoundingBox box;
   try {
     builder(items, rng, nodes_, box);
   } catch (...) {
-    objects_ = std::move(items);  // the world is unchanged by a failed build
+    // the world is unchanged by a failed build: objects, nodes and the scene
+    // stream (so a host build after it draws the reference's axes)
+    objects_ = std::move(items);
+    nodes_.resize(root);
+    rng = saved_rng;
     throw;
   }
   objects_.push_back(Item{MRT_REF(MRT_REF_NODE, root), box});

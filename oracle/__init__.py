@@ -33,7 +33,7 @@ def lib() -> C.CDLL:
         build()
     L = C.CDLL(str(LIB))
     P, U32, U64, F, I, I64 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_float, C.c_int, C.c_int64
-    fp, up = C.POINTER(C.c_float), C.POINTER(C.c_uint32)
+    fp, up, dp = C.POINTER(C.c_float), C.POINTER(C.c_uint32), C.POINTER(C.c_double)
     sig = {
         "orc_last_error": (C.c_char_p, []),
         "orc_new": (P, [U64]),
@@ -74,6 +74,7 @@ def lib() -> C.CDLL:
         "orc_tonemap": (I, [U32, U32, fp, up, U32, U32, C.POINTER(C.c_uint8)]),
         "orc_tonemap_check": (U64, [up, I]),
         "orc_prepass": (I, [P, U32, U32, U64, I, fp, fp]),
+        "orc_render_refrng": (I, [P, U32, U32, U32, U64, U32, U32, I, dp, dp, dp, dp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -292,6 +293,20 @@ class Scene:
         if secs < 0:
             raise OracleError("reference-mode bench failed")
         return secs, rgb, b
+
+    def render_refrng(self, width, height, passes, workers, seed=1, max_depth=50, threads=0):
+        """Reference RNG semantics (one fastrand stream per worker, pixel-loop
+        order): sums and sums of squares of the radiance [H*W*3] and of the
+        bounce counts [H*W] over passes x workers samples per pixel (float64)."""
+        s = np.zeros(width * height * 3)
+        q = np.zeros(width * height * 3)
+        b = np.zeros(width * height)
+        bq = np.zeros(width * height)
+        dp = C.POINTER(C.c_double)
+        self._chk(lib().orc_render_refrng(self.h, width, height, passes, seed, max_depth, workers, threads,
+                                          s.ctypes.data_as(dp), q.ctypes.data_as(dp), b.ctypes.data_as(dp),
+                                          bq.ctypes.data_as(dp)))
+        return s, q, b, bq
 
     def counters(self) -> dict:
         c = _Counters()

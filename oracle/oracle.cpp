@@ -186,10 +186,11 @@ struct Counters {
   }
 };
 struct Ctx {
-  PathRng* rng = nullptr;
+  PathRng* rng = nullptr;  // per-(pixel, sample) stream (the GPU's)
+  Wy* wy = nullptr;        // or one worker-wide fastrand stream (the reference's, orc_render_refrng)
   Counters cnt;
   bool in_alpha = false;
-  float rand() { return rng->f32(); }
+  float rand() { return wy ? wy->f32() : rng->f32(); }
 };
 
 // math.rs:262-287
@@ -1668,11 +1669,24 @@ static void sample_pixel(const orc_scene* s, uint32_t W, uint32_t H, uint32_t p,
   c.cnt.samples++;
 }
 
-static void run_threads(int threads, uint32_t n, const std::function<void(uint32_t, uint32_t)>& body) {
+// main.rs:258-263 with the reference's RNG: every draw from the worker's one
+// thread-local fastrand stream (math.rs:244-246), in call order
+static void sample_pixel_wy(const orc_scene* s, uint32_t W, uint32_t H, uint32_t x, uint32_t y, uint32_t max_depth,
+                            Ctx& c, V3& color, uint32_t& bounces) {
+  float u = ((float)x + c.rand()) / (float)(W - 1);
+  float v = ((float)y + c.rand()) / (float)(H - 1);
+  Ray ray = s->camera.ray(u, v, c);
+  auto r = trace(s->world, ray, max_depth, c);
+  color = r.first;
+  bounces = max_depth - r.second;
+  c.cnt.samples++;
+}
+
+static void run_threads(int threads, uint32_t n, const std::function<void(uint32_t, uint32_t)>& body,
+                        uint32_t chunk = 64) {
   if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
   std::atomic<uint32_t> next{0};
   std::vector<std::thread> ts;
-  const uint32_t chunk = 64;
   for (int t = 0; t < threads; ++t)
     ts.emplace_back([&] {
       for (;;) {
@@ -1739,6 +1753,47 @@ int orc_render(orc_scene* s, uint32_t W, uint32_t H, uint32_t spp_begin, uint32_
       for (int k = 0; k < 3; ++k) rgb[3 * (size_t)px[i] + k] = o[3 * i + k];
       b[px[i]] = ob[i];
     }
+    return 0;
+  });
+}
+
+int orc_render_refrng(orc_scene* s, uint32_t W, uint32_t H, uint32_t passes, uint64_t seed, uint32_t max_depth,
+                      uint32_t workers, int threads, double* sum, double* sumsq, double* bsum, double* bsumsq) {
+  return guard([&] {
+    if (workers == 0) workers = 1;
+    const size_t n = (size_t)W * H;
+    std::exception_ptr err;
+    std::mutex mu;
+    run_threads(threads, workers, [&](uint32_t b, uint32_t e) {
+      std::vector<double> ls(3 * n, 0.0), lq(3 * n, 0.0), lb(n, 0.0), lbq(n, 0.0);
+      Ctx c;
+      try {
+        for (uint32_t w = b; w < e; ++w) {
+          uint64_t x = seed ^ ((uint64_t)w << 32);
+          Wy rng{sm64(x)};  // the reference seeds it from the clock and the thread id
+          c.wy = &rng;
+          for (uint32_t k = 0; k < passes; ++k)
+            for (uint32_t y = 0; y < H; ++y)  // main.rs:253-264: rows, then columns
+              for (uint32_t xx = 0; xx < W; ++xx) {
+                V3 col;
+                uint32_t bo;
+                sample_pixel_wy(s, W, H, xx, y, max_depth, c, col, bo);
+                const size_t p = (size_t)y * W + xx;
+                const double v[3] = {col.x, col.y, col.z};
+                for (int ch = 0; ch < 3; ++ch) ls[3 * p + ch] += v[ch], lq[3 * p + ch] += v[ch] * v[ch];
+                lb[p] += bo;
+                lbq[p] += (double)bo * bo;
+              }
+        }
+      } catch (...) {
+        std::lock_guard<std::mutex> g(mu);
+        err = std::current_exception();
+      }
+      std::lock_guard<std::mutex> g(mu);
+      for (size_t i = 0; i < 3 * n; ++i) sum[i] += ls[i], sumsq[i] += lq[i];
+      for (size_t i = 0; i < n; ++i) bsum[i] += lb[i], bsumsq[i] += lbq[i];
+    }, 1);
+    if (err) std::rethrow_exception(err);
     return 0;
   });
 }

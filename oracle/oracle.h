@@ -99,6 +99,16 @@ int orc_render_pixels(orc_scene* s, uint32_t W, uint32_t H, const uint32_t* pixe
 double orc_bench_reference_mode(orc_scene* s, uint32_t W, uint32_t H, uint32_t passes_per_thread, uint64_t seed,
                                 uint32_t max_depth, int threads, float* accum_rgb, uint32_t* accum_bounces,
                                 uint32_t row_begin, uint32_t row_end, uint32_t row_step);
+// The reference's RNG semantics (statistical check): each
+// of `workers` render threads owns ONE fastrand wyrand stream (the reference
+// seeds it from the clock and thread id, main.rs:245-250 + fastrand; here
+// splitmix64(seed ^ worker << 32)) and renders `passes` whole 1-spp passes in
+// the reference's loop order (main.rs:253-264), every draw — jitter u, v,
+// Camera::ray's disk, scatter, Volume / alpha draws — taken from that one
+// stream in call order (math.rs:244-246). Adds per-pixel sums and sums of
+// squares of the radiance (W*H*3 doubles each) and of the bounce counts (W*H).
+int orc_render_refrng(orc_scene* s, uint32_t W, uint32_t H, uint32_t passes, uint64_t seed, uint32_t max_depth,
+                      uint32_t workers, int threads, double* sum, double* sumsq, double* bsum, double* bsumsq);
 void orc_wyrand(uint64_t seed, uint32_t n, uint64_t* out_u64, float* out_f32);
 void orc_path_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint64_t* out_u64, float* out_f32);
 // Image::to_rgb_bytes (main.rs:640-722) + dump's row flip (main.rs:760-767):

@@ -185,3 +185,78 @@ def test_device_build_builtin_scenes(ctx, name, assets_dir):
     assert h.rand_f32() == b.rand_f32()
     host_ms, dev_ms = b.last_build_ms()
     assert host_ms >= 0 and dev_ms > 0
+
+
+@pytest.mark.gpu
+def test_failed_device_build_leaves_world_unchanged(ctx):
+    """A device build that fails (a NaN sort key in a node of >= 3 items) must
+    leave the world and the scene stream as they were: the host build after it
+    is the reference's tree and draws the same axes."""
+    def world(x):
+        m = x.material(1 if isinstance(x, oracle.Scene) else massrt.MAT_LAMBERTIAN, x.solid(1, 1, 1))
+        for k in range(9):
+            x.add_sphere(m, (float(k), 0.5 * k, -1.0 * k), 0.7)
+        x.add_sphere(m, (float("nan"),) * 3, 1.0)
+        return x
+
+    b, o = world(massrt.Builder(3)), world(oracle.Scene(3))
+    with pytest.raises(massrt.MassrtError, match="NaN"):
+        b.build_bvh_device(ctx)
+    b.build_bvh()
+    o.build_bvh()
+    assert_same_tree(b, o)
+    assert b.rand_f32() == o.rand_f32()
+
+
+@pytest.mark.gpu
+def test_device_build_two_items_with_nan_key(ctx):
+    """2 items: the reference compares once (a NaN compares false: the first
+    item goes left, geom.rs:122-129); the device build must agree, not fail."""
+    for first_nan in (True, False):
+        b, o = massrt.Builder(4), oracle.Scene(4)
+        mb, mo = b.material(massrt.MAT_LAMBERTIAN, b.solid(1, 1, 1)), o.material(1, o.solid(1, 1, 1))
+        centers = [(float("nan"),) * 3, (1.0, 2.0, 3.0)]
+        if not first_nan:
+            centers.reverse()
+        for c in centers:
+            b.add_sphere(mb, c, 1.0)
+            o.add_sphere(mo, c, 1.0)
+        b.build_bvh_device(ctx)
+        o.build_bvh()
+        lst, boxes = massrt.preorder(b.desc_only())
+        k, bx = o.preorder()
+        assert [tuple(x) for x in k.tolist()] == lst
+        assert b.rand_f32() == o.rand_f32()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_device_build_signed_zeros(ctx, seed):
+    """Keys of -0.0 and +0.0 (one key: `<` cannot order them) and node boxes
+    whose join picks between -0 and +0: device tree == host tree == oracle,
+    boxes compared as bits."""
+    rng = np.random.default_rng(seed)
+    vals = np.array([-0.0, 0.0, 1.0, -1.0], dtype=np.float32)
+    items = [(tuple(float(v) for v in rng.choice(vals, 3)), float(rng.choice([0.0, 1.0]))) for _ in range(300)]
+
+    def world(x, lam):
+        m = x.material(lam, x.solid(1, 1, 1))
+        for c, r in items:
+            x.add_sphere(m, c, r)
+        return x
+
+    h = world(massrt.Builder(seed), massrt.MAT_LAMBERTIAN)
+    d = world(massrt.Builder(seed), massrt.MAT_LAMBERTIAN)
+    o = world(oracle.Scene(seed), 1)
+    h.build_bvh()
+    d.build_bvh_device(ctx)
+    o.build_bvh()
+    assert_same_tree(h, o)
+    assert_same_tree(d, o)
+    lh, bh = massrt.preorder(h.desc_only())
+    ld, bd = massrt.preorder(d.desc_only())
+    assert lh == ld
+    ph = np.array([x for x in bh if x is not None], dtype=np.float32)
+    pd = np.array([x for x in bd if x is not None], dtype=np.float32)
+    assert np.array_equal(ph.view(np.uint32), pd.view(np.uint32))
+    assert (np.signbit(ph) & (ph == 0)).any() and (~np.signbit(ph) & (ph == 0)).any()  # both zeros occur

@@ -40,3 +40,47 @@ def test_fullsize_deterministic_and_shard_additive(ctx, grid):
         acc = ctx.render(W, H, 0, 2, seed=9, shard_index=i, shard_count=4, accum=acc)
     assert np.array_equal(a[0].view(np.uint32), acc[0].view(np.uint32))
     assert np.array_equal(a[1], acc[1])
+
+
+# ---- BASELINE config 5 size: textured 1M-triangle mesh + SkySphere env map at 3840x2160
+W4, H4 = 3840, 2160
+
+
+@pytest.fixture(scope="module")
+def textured(assets_dir):
+    return (massrt.Builder(1).builtin("mesh_obj_textured", ASPECT, assets_dir),
+            oracle.Scene(1).builtin("mesh_obj_textured", ASPECT, assets_dir))
+
+
+def test_4k_pixel_subset_across_result_chunks(ctx, textured):
+    """64 spp of the 4K frame = 531M samples: the library splits them into
+    result-slab chunks (256M samples, i.e. 30 spp of 8.3M pixels), so this
+    crosses two chunk boundaries. A pixel subset must match the oracle
+    (bounces bit-exact; radiance within 1e-4: acos/atan2 of SkySphere are
+    ocml vs glibc ULPs), and splitting the call at the chunk boundary must
+    not change a bit."""
+    b, o = textured
+    ctx.upload(b)
+    spp = 64
+    rgb, bo = ctx.render(W4, H4, 0, spp, seed=5)
+    px = np.arange(3, W4 * H4, 15_013, dtype=np.uint32)
+    orgb, obo = o.render_pixels(W4, H4, px, 0, spp, seed=5)
+    assert np.array_equal(bo[px], obo)
+    a = rgb.reshape(-1, 3)[px].astype(np.float64)
+    assert np.linalg.norm(a - orgb.reshape(-1, 3)) / np.linalg.norm(orgb) <= 1e-4
+    part = ctx.render(W4, H4, 0, 30, seed=5)
+    part = ctx.render(W4, H4, 30, spp - 30, seed=5, accum=part)
+    assert np.array_equal(rgb.view(np.uint32), part[0].view(np.uint32)) and np.array_equal(bo, part[1])
+
+
+def test_4k_deterministic_and_shard_additive(ctx, textured):
+    b, _ = textured
+    ctx.upload(b)
+    a = ctx.render(W4, H4, 0, 2, seed=6)
+    again = ctx.render(W4, H4, 0, 2, seed=6)
+    assert np.array_equal(a[0].view(np.uint32), again[0].view(np.uint32)) and np.array_equal(a[1], again[1])
+    acc = (np.zeros(W4 * H4 * 3, np.float32), np.zeros(W4 * H4, np.uint32))
+    for i in range(3):
+        acc = ctx.render(W4, H4, 0, 2, seed=6, shard_index=i, shard_count=3, accum=acc)
+    assert np.array_equal(a[0].view(np.uint32), acc[0].view(np.uint32))
+    assert np.array_equal(a[1], acc[1])
