@@ -10,7 +10,8 @@ and averaged over dispatches. Derived for k_trace:
   l1_hit    = 1 - TCP_TCC_READ_REQ_sum / TCP_TOTAL_CACHE_ACCESSES_sum
   l2_hit    = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
   wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES
-  valu_busy = SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE/8) / (4 SIMDs x CUs)
+  valu_busy = 2 * SQ_INSTS_VALU / (GRBM_GUI_ACTIVE/8) / (4 SIMDs x CUs)
+              (a wave64 VALU instruction occupies a SIMD-32 for 2 cycles)
   lds_busy  = SQ_LDS_IDX_ACTIVE / (GRBM_GUI_ACTIVE/8) / CUs
 The stamp (scene, size, spp per step, source hash) ties the file to the code
 and configuration it measured; bench.py ignores a file whose stamp differs.
@@ -88,8 +89,8 @@ for name, k in summary["kernels"].items():
     if k.get("SQ_WAVE_CYCLES"):
         k["wait_frac"] = k.get("SQ_WAIT_ANY", 0) / k["SQ_WAVE_CYCLES"]
     g2 = k.get("GRBM_GUI_ACTIVE_sq2")
-    if g2 and "SQ_ACTIVE_INST_VALU" in k:
-        k["valu_busy"] = k["SQ_ACTIVE_INST_VALU"] / (g2 / N_XCD) / (4 * N_CU)
+    if g and "SQ_INSTS_VALU" in k:
+        k["valu_busy"] = 2 * k["SQ_INSTS_VALU"] / (g / N_XCD) / (4 * N_CU)
     if g2 and "SQ_LDS_IDX_ACTIVE" in k:
         k["lds_busy"] = k["SQ_LDS_IDX_ACTIVE"] / (g2 / N_XCD) / N_CU
     if k.get("SQ_WAVES") and "SQ_INSTS_VALU" in k:
