@@ -19,6 +19,7 @@ Usage: python tools/gen_assets.py [--out assets] [--all]
 from __future__ import annotations
 
 import argparse
+import os
 import io
 import shutil
 from pathlib import Path
@@ -178,26 +179,37 @@ def ensure_environment(out: Path, name: str = "j02"):
 
 def ensure_assets(out: Path | str = DEFAULT_DIR, mesh: bool = True, textures: bool = False,
                   environment: bool = False) -> Path:
+    """Generate the missing assets under `out`. Safe to call from several
+    processes at once (pytest -n, ranks): one holds an exclusive lock while it
+    writes, every file appears by rename only when complete."""
+    import fcntl
+
     out = Path(out)
     out.mkdir(parents=True, exist_ok=True)
-    if not (out / "cube.ply").exists():
-        shutil.copy(REPO / "tests" / "golden" / "cube.ply", out / "cube.ply")
+    with open(out / ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        _ensure_locked(out, mesh, textures, environment)
+    return out
+
+
+def _ensure_locked(out: Path, mesh: bool, textures: bool, environment: bool) -> None:
+    def publish(name, write):
+        if not (out / name).exists():
+            tmp = out / f".tmp{os.getpid()}_{name}"
+            write(tmp)
+            tmp.rename(out / name)
+
+    publish("cube.ply", lambda p: shutil.copy(REPO / "tests" / "golden" / "cube.ply", p))
     if environment:
         ensure_environment(out)
     if mesh and not ((out / "mesh_1m.ply").exists() and (out / "mesh_1m.obj").exists()):
         P, N, UV = torus_grid()
         F = torus_faces()
-        write_ply(out / "mesh_1m.ply.tmp", P.reshape(-1, 3), F)
-        (out / "mesh_1m.ply.tmp").rename(out / "mesh_1m.ply")
-        write_obj(out / "mesh_1m.obj.tmp", P.reshape(-1, 3), N.reshape(-1, 3), UV.reshape(-1, 2), F)
-        (out / "mesh_1m.obj.tmp").rename(out / "mesh_1m.obj")
+        publish("mesh_1m.ply", lambda p: write_ply(p, P.reshape(-1, 3), F))
+        publish("mesh_1m.obj", lambda p: write_obj(p, P.reshape(-1, 3), N.reshape(-1, 3), UV.reshape(-1, 2), F))
     if textures:
-        if not (out / "albedo_2048.png").exists():
-            write_png(out / "albedo_2048.png", albedo())
-        if not (out / "env_4096x2048.png").exists():
-            write_png(out / "env_4096x2048.png", env())
-    return out
-
+        publish("albedo_2048.png", lambda p: write_png(p, albedo()))
+        publish("env_4096x2048.png", lambda p: write_png(p, env()))
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
