@@ -908,7 +908,7 @@ struct mrt_ctx {
   // global load of a step only when every lane of the wave is in the copy,
   // and the TA cost is per wave instruction, not per lane — 256/16 KB and
   // 1024/78 KB were 1% and 1-4% slower than no treelet.
-  int trace_block = 256;           // k_trace workgroup size with a treelet (MRT_TRACE_BLOCK: 256 or 1024)
+  int trace_block = 256;           // k_trace workgroup size with a treelet (MRT_TRACE_BLOCK: 256, 512 or 1024)
   uint32_t treelet_kb = 0;         // treelet budget per workgroup (MRT_TREELET_KB; 0 = none)
 
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t*, uint32_t>> pixlists;
@@ -1013,6 +1013,8 @@ void launch_trace_r(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& 
     launch_trace_b<false, ALPHA, RNG, kBlock>(c, st, q, in, cur, count, tmin, tmax);
   else if (c->trace_block == 1024)
     launch_trace_b<true, ALPHA, RNG, 1024>(c, st, q, in, cur, count, tmin, tmax);
+  else if (c->trace_block == 512)
+    launch_trace_b<true, ALPHA, RNG, 512>(c, st, q, in, cur, count, tmin, tmax);
   else
     launch_trace_b<true, ALPHA, RNG, kBlock>(c, st, q, in, cur, count, tmin, tmax);
 }
@@ -1404,7 +1406,7 @@ int mrt_create(int device, mrt_ctx** out) {
     if (const char* e = getenv("MRT_POOL_PATHS")) c->pool_paths = (size_t)std::max(1 << 16, std::min(1 << 28, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_BLOCK")) {
       const int b = atoi(e);
-      c->trace_block = b >= 1024 ? 1024 : 256;
+      c->trace_block = b >= 1024 ? 1024 : (b >= 512 ? 512 : 256);
     }
     if (const char* e = getenv("MRT_TREELET_KB")) c->treelet_kb = (uint32_t)std::max(0, std::min(150, atoi(e)));
   });

@@ -84,3 +84,26 @@ def test_4k_deterministic_and_shard_additive(ctx, textured):
         acc = ctx.render(W4, H4, 0, 2, seed=6, shard_index=i, shard_count=3, accum=acc)
     assert np.array_equal(a[0].view(np.uint32), acc[0].view(np.uint32))
     assert np.array_equal(a[1], acc[1])
+
+
+@pytest.mark.parametrize("scene", ["sphere_grid", "cube_field", "mesh_ply"])
+def test_fullsize_treelet_equals_plain(golden_dir, assets_dir, monkeypatch, scene):
+    """k_trace with the LDS treelet and parked global loads (1024 threads,
+    78 KB) renders full 1080p frames bit-identical to the plain kernel: many
+    refills per lane, both queues, every lane state transition at scale."""
+    b = massrt.Builder(1).builtin(scene, ASPECT, assets_dir if scene == "mesh_ply" else golden_dir)
+    spp = 1 if scene == "mesh_ply" else 2
+    out = []
+    for block, kb in ((256, 0), (1024, 78)):
+        monkeypatch.setenv("MRT_TRACE_BLOCK", str(block))
+        monkeypatch.setenv("MRT_TREELET_KB", str(kb))
+        c = massrt.Context(0)
+        try:
+            c.upload(b)
+            out.append(c.render(W, H, 0, spp, seed=5))
+            if massrt.lib().mrt_debug_build():  # MASSRT_LIB=dbg: no index out of range
+                assert c.debug_status()[3] == 0, c.debug_status()
+        finally:
+            c.close()
+    assert np.array_equal(out[0][1], out[1][1])
+    assert np.array_equal(out[0][0].view(np.uint32), out[1][0].view(np.uint32))

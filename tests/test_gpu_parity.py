@@ -554,7 +554,7 @@ def test_menger_parity(ctx, assets_dir, scene):
         assert bo.mean() / spp > 1.0  # the sponge and the ground are in view
 
 
-@pytest.mark.parametrize("block,kb", [(256, 0), (256, 1), (256, 4), (256, 24), (1024, 78), (1024, 150)])
+@pytest.mark.parametrize("block,kb", [(256, 0), (256, 1), (256, 4), (256, 24), (512, 48), (1024, 78), (1024, 150)])
 def test_treelet_budgets_bit_exact(golden_dir, monkeypatch, block, kb):
     """The LDS treelet (upload.cpp build_treelet) at several budgets and
     workgroup sizes: no treelet, a few boxes, the top of the trees, small
