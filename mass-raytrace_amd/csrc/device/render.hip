@@ -903,6 +903,7 @@ struct mrt_ctx {
   size_t pool_paths = (size_t)128 << 20;
   int cus = 1;
   bool trace_lds = false;          // the scene has an LDS treelet (set per scene)
+  bool tune_auto_loop = true;      // refill/box_min chosen per scene (unless MRT_TRACE_REFILL/BOX_MIN set)
   uint32_t tl_boxes = 0;           // box records in the treelet
   // LDS treelet: off by default. Measured: it removes the
   // global load of a step only when every lane of the wave is in the copy,
@@ -1398,6 +1399,7 @@ int mrt_create(int device, mrt_ctx** out) {
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     c->cus = std::max(1, cus);
     c->trace_grid = (uint32_t)c->cus * 4;  // k_trace_simple (debug)
+    if (getenv("MRT_TRACE_REFILL") || getenv("MRT_TRACE_BOX_MIN")) c->tune_auto_loop = false;
     if (const char* e = getenv("MRT_TRACE_REFILL")) c->tune.refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_PRIM_BATCH")) c->tune.prim_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_CHUNK")) c->tune.chunk = (uint32_t)std::max(64, atoi(e));
@@ -1555,6 +1557,18 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     c->S = S;
     c->scene_bytes = off;
     c->trace_lds = S.n_tlet > 0;
+    // Persistent-loop thresholds per scene (profiles/r2_tune):
+    // a record stream larger than half the chip's L2 (32 MiB over 8 XCDs)
+    // misses to the Infinity Cache, each load round trip is longer, and it
+    // pays to keep more lanes per load instruction (box run while >= 32 lanes
+    // are at a box) and to refill sooner: mesh_ply 438 -> 458, Menger 37.1 ->
+    // 38.2 Msamples/s; L2-resident streams keep 32/24 (sphere_grid 640 vs
+    // 609, cube_field 252 vs 246).
+    if (c->tune_auto_loop) {
+      const bool big = (size_t)S.n_slots * 16 > ((size_t)16 << 20);
+      c->tune.refill = big ? 16u : 32u;
+      c->tune.box_min = big ? 32u : 24u;
+    }
     c->tl_boxes = hs.tl_boxes;
     c->scene_alpha = hs.has_alpha;
     c->scene_rng = hs.trav_rng;
