@@ -353,6 +353,8 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
             "achieved_per_step": round(bytes_per_seg * segs / elapsed / 1e9, 1),
             "bytes_per_segment": round(bytes_per_seg, 1), "segments_per_sample": round(seg_per_sample, 4),
             "lane_utilisation": round(cnt["lane_steps"] / max(cnt["wave_slots"], 1), 4),
+            # box tests the early slab decision left to the exact test (path.h box_hit_any)
+            "box_exact_frac": round(cnt.get("box_exact", 0) / max(cnt["node_visits"], 1), 5),
         }
 
     out = {"scene": scene, "value": round(value, 3), "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps,

@@ -1,4 +1,4 @@
-//! Raw FFI of include/massrt.h, MRT_ABI_VERSION 5.
+//! Raw FFI of include/massrt.h, MRT_ABI_VERSION 6.
 //!
 //! Every struct is `#[repr(C)]` with the header's field order and types;
 //! tests/test_rust_binding.py parses this file and checks each struct's
@@ -8,7 +8,7 @@
 
 use std::os::raw::{c_char, c_void};
 
-pub const MRT_ABI_VERSION: i32 = 5;
+pub const MRT_ABI_VERSION: i32 = 6;
 
 pub const MRT_OK: i32 = 0;
 pub const MRT_ERR_INVALID: i32 = 1;
@@ -260,6 +260,7 @@ pub struct mrt_counters {
     pub bounces: u64,
     pub wave_slots: u64,
     pub lane_steps: u64,
+    pub box_exact: u64,
 }
 
 #[repr(C)]

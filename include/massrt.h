@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 5
+#define MRT_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------ */
 #define MRT_OK 0
@@ -251,6 +251,8 @@ typedef struct {
    * executed; lane_steps / wave_slots = SIMD lane utilisation */
   uint64_t wave_slots;
   uint64_t lane_steps;
+  /* box tests the early slab decision left to the exact slab test (ABI v6) */
+  uint64_t box_exact;
 } mrt_counters;
 
 /* Kernel timing accumulated by renders flagged MRT_RENDER_TIME_KERNELS

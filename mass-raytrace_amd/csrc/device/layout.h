@@ -103,7 +103,8 @@ struct DevScene {
   const GpuMaterial* materials;
   const GpuTexture* textures;
   const uint32_t* texels;  // RGBA8 packed little-endian
-  uint32_t fast_ok;  // every box coordinate in {0} U [2^-40, 2^28] (path.h div fast path)
+  uint32_t fast_ok;  // bit 0: every box coordinate in {0} U [2^-40, 2^28] (path.h qfast exact test);
+                     // bit 1: every box coordinate finite, |c| <= 2^28 (path.h early slab decision)
   // array sizes (checked only in MRT_DEBUG_BOUNDS builds) and the debug record
   uint32_t n_slots, n_tris, n_sph, n_inst, n_models, n_materials, n_textures, n_texels;
   uint32_t* dbg;  // {first failing check code, index, bound, failures}

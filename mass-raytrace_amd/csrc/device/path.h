@@ -27,12 +27,12 @@ MRT_DEV uint32_t make_ref(uint32_t kind, uint32_t idx) { return (kind << 28) | i
 
 struct DevCounters {
   unsigned long long samples, segments, node_visits, sphere_tests, triangle_tests, instance_entries,
-      model_entries, closest_hits, texel_taps, bounces, wave_slots, lane_steps;
+      model_entries, closest_hits, texel_taps, bounces, wave_slots, lane_steps, box_exact;
 };
 
 struct LocalCounters {
   uint32_t node_visits = 0, sphere_tests = 0, triangle_tests = 0, instance_entries = 0, model_entries = 0,
-           texel_taps = 0, wave_slots = 0, lane_steps = 0;
+           texel_taps = 0, wave_slots = 0, lane_steps = 0, box_exact = 0;
 };
 
 // Bounds checks of every scene-array index, compiled in with
@@ -195,24 +195,36 @@ struct TRay {
   V3 o, d;
   float yx, yy, yz;
   float oyx, oyy, oyz;  // RN(o.k * y.k)
-  float om;             // max_k |oy.k| * 2^-20 (box_hit_any)
+  // |om| = max(max_k |oy.k| * 2^-20, 2^-120), the early decision's absolute
+  // margin term (box_hit_any); its sign bit set: the exact test may NOT use
+  // qfast (the ray or the scene is outside the qfast domain below)
+  float om;
   Recip a;    // |d|^2 for Sphere::intersect
-  bool fast;  // every slab quotient of this ray can take div_fast exactly
+  bool fast;  // the early slab decision applies to this ray (early domain below)
 };
-// Fast-path domain: with every box coordinate and ray-origin coordinate in
+// qfast domain: with every box coordinate and ray-origin coordinate in
 // {0} U [2^-40, 2^28] (scene bound checked on the host, origin here) each
 // nonzero numerator (min - o) is >= 2^-63 and < 2^29; with |d| in
 // [2^-20, 2^20] every quotient lies in [2^-83, 2^49] — inside div_fast's
 // exact range — so no per-quotient check is needed.
+// Early domain (slab_fast): its error bound needs no lower bound on the
+// coordinates, only that no product overflows — box and origin coordinates
+// finite and within 2^28, |d| in [2^-20, 2^20] — plus an absolute 2^-149 per
+// rounding in the subnormal range, which the 2^-120 floor of |om| covers. (A
+// mesh vertex at sin(pi) ~ 1e-16 is outside the qfast domain; until round 2's
+// split it switched the whole 1M-triangle mesh_ply scene to the exact test.)
 MRT_DEV bool coord_ok(float c) {
   float a = fabsf(c);
   return a == 0.0f || (a >= 0x1p-40f && a <= 0x1p28f);
 }
+MRT_DEV bool orig_ok(float c) { return fabsf(c) <= 0x1p28f; }
 MRT_DEV bool dir_ok(float c) {
   float a = fabsf(c);
   return a >= 0x1p-20f && a <= 0x1p20f;
 }
-MRT_DEV TRay make_tray(V3 o, V3 d, bool scene_fast) {
+// scene_flags (DevScene::fast_ok): bit 0 every box coordinate in the qfast
+// domain, bit 1 every box coordinate finite and within 2^28.
+MRT_DEV TRay make_tray(V3 o, V3 d, uint32_t scene_flags) {
   TRay r;
   r.o = o;
   r.d = d;
@@ -222,10 +234,12 @@ MRT_DEV TRay make_tray(V3 o, V3 d, bool scene_fast) {
   r.oyx = o.x * r.yx;
   r.oyy = o.y * r.yy;
   r.oyz = o.z * r.yz;
-  r.om = fmaxf(fmaxf(fabsf(r.oyx), fabsf(r.oyy)), fabsf(r.oyz)) * 0x1p-20f;
+  const float om = fmaxf(fmaxf(fmaxf(fabsf(r.oyx), fabsf(r.oyy)), fabsf(r.oyz)) * 0x1p-20f, 0x1p-120f);
   r.a = make_recip(length_squared(d));
-  r.fast = scene_fast && coord_ok(o.x) && coord_ok(o.y) && coord_ok(o.z) && dir_ok(d.x) && dir_ok(d.y) &&
-           dir_ok(d.z);
+  const bool dok = dir_ok(d.x) && dir_ok(d.y) && dir_ok(d.z);
+  const bool qok = (scene_flags & 1u) && coord_ok(o.x) && coord_ok(o.y) && coord_ok(o.z) && dok;
+  r.om = qok ? om : -om;
+  r.fast = (scene_flags & 2u) && orig_ok(o.x) && orig_ok(o.y) && orig_ok(o.z) && dok;
   return r;
 }
 MRT_DEV float qfast(float a, float b, float y) {
@@ -443,7 +457,7 @@ MRT_DEV bool box_hit_exact(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) 
   V3 na = mn - r.o, nb = mx - r.o;
   V3 a{qfast(na.x, r.d.x, r.yx), qfast(na.y, r.d.y, r.yy), qfast(na.z, r.d.z, r.yz)};
   V3 b{qfast(nb.x, r.d.x, r.yx), qfast(nb.y, r.d.y, r.yy), qfast(nb.z, r.d.z, r.yz)};
-  if (!r.fast) {
+  if (signbit(r.om)) {  // outside the qfast domain
     a = na / r.d;
     b = nb / r.d;
   }
@@ -458,7 +472,7 @@ MRT_DEV bool box_hit_exact(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) 
 // one in the FMA, half an ulp to the quotient; no under/overflow in the fast
 // domain. min/max are 1-Lipschitz and the terms that decide them lie at t0
 // (t1), so t0 and t1 carry that bound relative to their own magnitude plus
-// max_k |o.k*y.k|*2^-23.9. When t1 - t0 exceeds (|t0|+|t1|)*2^-19 + om (om =
+// max_k |o.k*y.k|*2^-23.9. When t1 - t0 exceeds (|t0|+|t1|)*2^-19 + |om| (|om| >=
 // max_k |o.k*y.k|*2^-20, 4x slack on both terms) the comparison of the exact
 // values is decided; otherwise — grazing rays, flat boxes, ties — the exact
 // test decides. mrt_selftest_slab checks this against box_hit_exact on
@@ -469,8 +483,11 @@ MRT_DEV void slab_fast(V3 mn, V3 mx, const TRay& r, float tmin, float tmax, floa
   t0 = vmax3(vmin1(ax, bx), vmin1(ay, by), vmax1(vmin1(az, bz), tmin));
   t1 = vmin3(vmax1(ax, bx), vmax1(ay, by), vmin1(vmax1(az, bz), tmax));
 }
-MRT_DEV float slab_margin(const TRay& r, float t0, float t1) { return fmaf(fabsf(t0) + fabsf(t1), 0x1p-19f, r.om); }
-MRT_DEV bool box_hit_any(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) {
+MRT_DEV float slab_margin(const TRay& r, float t0, float t1) {
+  return fmaf(fabsf(t0) + fabsf(t1), 0x1p-19f, fabsf(r.om));
+}
+template <bool COUNT = false>
+MRT_DEV bool box_hit_any(V3 mn, V3 mx, const TRay& r, float tmin, float tmax, LocalCounters* lc = nullptr) {
   if (r.fast) {
     float t0, t1;
     slab_fast(mn, mx, r, tmin, tmax, t0, t1);
@@ -482,6 +499,7 @@ MRT_DEV bool box_hit_any(V3 mn, V3 mx, const TRay& r, float tmin, float tmax) {
     if (gap > m) return true;
     if (-gap > m) return false;
   }
+  if (COUNT) lc->box_exact++;
   return box_hit_exact(mn, mx, r, tmin, tmax);
 }
 
@@ -546,7 +564,7 @@ template <bool COUNT, bool LDS = false>
 MRT_DEV void trav_box(const TravIn& in, Trav& t, LocalCounters& lc) {
   if (COUNT) lc.node_visits++;
   V3 mn{u2f(t.s0.x), u2f(t.s0.y), u2f(t.s0.z)}, mx{u2f(t.s0.w), u2f(t.s1.x), u2f(t.s1.y)};
-  t.i = box_hit_any(mn, mx, t.r, in.tmin, t.best) ? (t.s1.w & ~kBoxFlag) : t.s1.z;
+  t.i = box_hit_any<COUNT>(mn, mx, t.r, in.tmin, t.best, &lc) ? (t.s1.w & ~kBoxFlag) : t.s1.z;
   trav_fetch<LDS>(in, t);
 }
 
@@ -560,7 +578,7 @@ MRT_DEV void trav_box_index(const TravIn& in, Trav& t, LocalCounters& lc) {
   for (int k = 0; k < MRT_PAD_VALU; ++k) asm volatile("v_nop");
 #endif
   V3 mn{u2f(t.s0.x), u2f(t.s0.y), u2f(t.s0.z)}, mx{u2f(t.s0.w), u2f(t.s1.x), u2f(t.s1.y)};
-  t.i = box_hit_any(mn, mx, t.r, in.tmin, t.best) ? (t.s1.w & ~kBoxFlag) : t.s1.z;
+  t.i = box_hit_any<COUNT>(mn, mx, t.r, in.tmin, t.best, &lc) ? (t.s1.w & ~kBoxFlag) : t.s1.z;
 }
 
 // The current record is a primitive, an instance or a model. ALPHA=false is

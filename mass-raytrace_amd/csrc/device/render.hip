@@ -115,11 +115,11 @@ __device__ __forceinline__ uint32_t wg_reserve(uint32_t* counter, uint32_t count
 
 __device__ void flush_counters(DevCounters* c, const LocalCounters& lc, uint32_t segs, uint32_t hits,
                                uint32_t samples, uint32_t bounces) {
-  uint32_t v[12] = {samples, segs, lc.node_visits, lc.sphere_tests, lc.triangle_tests, lc.instance_entries,
-                    lc.model_entries, hits, lc.texel_taps, bounces, lc.wave_slots, lc.lane_steps};
+  uint32_t v[13] = {samples, segs, lc.node_visits, lc.sphere_tests, lc.triangle_tests, lc.instance_entries,
+                    lc.model_entries, hits, lc.texel_taps, bounces, lc.wave_slots, lc.lane_steps, lc.box_exact};
   unsigned long long* dst = reinterpret_cast<unsigned long long*>(c);
 #pragma unroll
-  for (int k = 0; k < 12; ++k) {
+  for (int k = 0; k < 13; ++k) {
     uint32_t s = wave_sum(v[k]);
     if (lane_id() == 0 && s) atomicAdd(dst + k, (unsigned long long)s);
   }
@@ -815,10 +815,17 @@ __global__ __launch_bounds__(kBlock) void k_selftest_slab(unsigned long long n, 
       mx[k] = fmaxf(lo, hi);
       if ((r >> 10 & 7) == 0) mx[k] = mn[k];  // flat box
     }
-    bool ok = true;
+    // every 8th case: some box minima replaced by a tiny nonzero coordinate
+    // (~1e-16, a mesh vertex at sin(pi)): outside the qfast domain, inside the
+    // early decision's; the exact test then divides
+    if ((sc >> 40 & 7) == 0)
+      for (int k = 0; k < 3; ++k)
+        if (rnd() & 1) mn[k] = fminf(mx[k], __uint_as_float((__float_as_uint(mn[k]) & 0x80000000u) | 0x25100000u));
+    bool ok = true, early = true;
     for (int k = 0; k < 3; ++k) ok = ok && coord_ok(mn[k]) && coord_ok(mx[k]);
-    if (!ok) continue;
-    const TRay ray = make_tray(o, d, true);
+    for (int k = 0; k < 3; ++k) early = early && orig_ok(mn[k]) && orig_ok(mx[k]);
+    if (!early) continue;
+    const TRay ray = make_tray(o, d, ok ? 3u : 2u);
     if (!ray.fast) continue;
     const uint64_t rt = rnd();
     const float tmin = (rt & 3) == 0 ? nudge(t, -(int)(rt >> 2 & 3)) : 0.001f;
@@ -1534,7 +1541,7 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     S.materials = (const GpuMaterial*)(base + o_mat);
     S.textures = (const GpuTexture*)(base + o_tex);
     S.texels = (const uint32_t*)(base + o_texel);
-    S.fast_ok = hs.fast_ok;
+    S.fast_ok = (hs.fast_ok ? 1u : 0u) | (hs.early_ok ? 2u : 0u);
     S.vol_nid = (const float*)(base + o_vnid);
     S.vol_mat = (const uint32_t*)(base + o_vmat);
     S.ln_table = ln_table.empty() ? nullptr : (const float*)(base + o_ln);
@@ -1688,6 +1695,7 @@ int mrt_get_counters(mrt_ctx* c, mrt_counters* out) {
     out->bounces = h.bounces;
     out->wave_slots = h.wave_slots;
     out->lane_steps = h.lane_steps;
+    out->box_exact = h.box_exact;
   });
 }
 

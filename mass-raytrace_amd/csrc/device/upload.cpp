@@ -270,6 +270,7 @@ struct Emitter {
         for (float v : c) {
           float a = fabsf(v);
           if (!(a == 0.0f || (a >= 0x1p-40f && a <= 0x1p28f))) s.fast_ok = 0;
+          if (!(a <= 0x1p28f)) s.early_ok = 0;  // NaN and inf too
         }
       }
       uint32_t at = push_slot(fbits(n.min[0]), fbits(n.min[1]), fbits(n.min[2]), fbits(n.max[0]));

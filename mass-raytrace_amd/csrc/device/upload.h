@@ -25,7 +25,8 @@ struct HostScene {
   std::vector<GpuMaterial> materials;
   std::vector<GpuTexture> textures;
   std::vector<uint32_t> texels;
-  uint32_t fast_ok = 1;
+  uint32_t fast_ok = 1;   // every box coordinate in {0} U [2^-40, 2^28]: the exact slab test may use qfast
+  uint32_t early_ok = 1;  // every box coordinate finite and within 2^28: the early slab decision applies
   bool has_alpha = false;  // some triangle carries TRI_FLAG_ALPHA
   bool trav_rng = false;   // the traversal draws random numbers (Volume, Mix alpha tests)
   std::vector<float> vol_nid;

@@ -1,0 +1,234 @@
+// slab_check — host-side restatement of k_trace's early slab decision
+// (path.h make_tray / slab_fast / box_hit_any), run over the record stream of
+// a built-in scene on camera rays and one-bounce rays, no GPU needed: every
+// box the early decision settles must get the exact BoundingBox::hit answer
+// (IEEE quotients, geom.rs:218-247), and the fraction left to the exact test
+// is reported. Round 2 used it to find that mesh_ply's vertices at ~1e-16
+// (sin(pi)) had switched the whole scene to the exact test.
+//   g++ -O2 -std=c++17 -ffp-contract=off -o tools/slab_check tools/slab_check.cpp -Lmass-raytrace_amd/massrt
+//       -lmassrt -Wl,-rpath,$PWD/mass-raytrace_amd/massrt && tools/slab_check mesh_ply 20000 assets
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../mass-raytrace_amd/csrc/device/upload.h"
+
+using namespace mrt;
+
+namespace {
+
+float f(uint32_t u) {
+  float x;
+  memcpy(&x, &u, 4);
+  return x;
+}
+struct V {
+  float x, y, z;
+};
+V sub(V a, V b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+float dot(V a, V b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+V cross(V a, V b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+
+struct Ray {
+  V o, d;
+  float y[3], oy[3], om;
+  bool fast;
+};
+bool dir_ok(float c) {
+  float a = fabsf(c);
+  return a >= 0x1p-20f && a <= 0x1p20f;
+}
+Ray make_ray(V o, V d, bool scene_fast) {
+  Ray r{o, d, {}, {}, 0, false};
+  const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+  float m = 0;
+  for (int k = 0; k < 3; ++k) {
+    r.y[k] = 1.0f / dd[k];
+    r.oy[k] = oo[k] * r.y[k];
+    m = std::max(m, fabsf(r.oy[k]));
+  }
+  r.om = std::max(m * 0x1p-20f, 0x1p-120f);
+  // early-decision domain (path.h make_tray): finite origin within 2^28, |d| in [2^-20, 2^20]
+  auto o_ok = [](float c) { return fabsf(c) <= 0x1p28f; };
+  r.fast = scene_fast && o_ok(o.x) && o_ok(o.y) && o_ok(o.z) && dir_ok(d.x) && dir_ok(d.y) && dir_ok(d.z);
+  return r;
+}
+// BoundingBox::hit with IEEE quotients (fminf/fmaxf = minNum/maxNum, as v_min/v_max)
+bool box_exact(const float mn[3], const float mx[3], const Ray& r, float tmin, float tmax) {
+  const float oo[3] = {r.o.x, r.o.y, r.o.z}, dd[3] = {r.d.x, r.d.y, r.d.z};
+  float t0 = tmin, t1 = tmax;
+  float a[3], b[3];
+  for (int k = 0; k < 3; ++k) a[k] = (mn[k] - oo[k]) / dd[k], b[k] = (mx[k] - oo[k]) / dd[k];
+  t0 = fmaxf(fmaxf(fminf(a[0], b[0]), fminf(a[1], b[1])), fmaxf(fminf(a[2], b[2]), tmin));
+  t1 = fminf(fminf(fmaxf(a[0], b[0]), fmaxf(a[1], b[1])), fminf(fmaxf(a[2], b[2]), tmax));
+  return !(t1 < t0);
+}
+float margin(const Ray& r, float t0, float t1) { return std::fma(fabsf(t0) + fabsf(t1), 0x1p-19f, r.om); }
+
+struct Stats {
+  uint64_t boxes = 0, undecided = 0, wrong = 0;
+};
+// path.h box_hit_any's early decision: 1 hit, 0 miss, -1 left to the exact test
+int early_decide(const float mn[3], const float mx[3], const Ray& r, float tmin, float best) {
+  if (!r.fast) return -1;
+  float a[3], b[3];
+  for (int k = 0; k < 3; ++k) a[k] = std::fma(mn[k], r.y[k], -r.oy[k]), b[k] = std::fma(mx[k], r.y[k], -r.oy[k]);
+  const float t0 = fmaxf(fmaxf(fminf(a[0], b[0]), fminf(a[1], b[1])), fmaxf(fminf(a[2], b[2]), tmin));
+  const float t1 = fminf(fminf(fmaxf(a[0], b[0]), fmaxf(a[1], b[1])), fminf(fmaxf(a[2], b[2]), best));
+  const float m = margin(r, t0, t1), gap = t1 - t0;
+  return gap > m ? 1 : (-gap > m ? 0 : -1);
+}
+
+bool sphere_hit(V c, float rad, V o, V d, float tmin, float tmax, float& t) {
+  V oc = sub(o, c);
+  float a = dot(d, d), hb = dot(oc, d), cc = dot(oc, oc) - rad * rad, disc = hb * hb - a * cc;
+  if (disc < 0.0f) return false;
+  float sq = sqrtf(disc), root = (-hb - sq) / a;
+  if (root < tmin || tmax < root) {
+    root = (-hb + sq) / a;
+    if (root < tmin || tmax < root) return false;
+  }
+  t = root;
+  return true;
+}
+bool tri_hit(V a, V ab, V ac, V o, V d, float tmin, float tmax, float& t) {
+  V p = cross(d, ac);
+  float det = dot(ab, p);
+  if (fabsf(det) < 0.000001f) return false;
+  float inv = 1.0f / det;
+  V tv = sub(o, a);
+  float u = dot(tv, p) * inv;
+  if (u < 0.0f || u > 1.0f) return false;
+  V qv = cross(tv, ab);
+  float v = dot(d, qv) * inv;
+  if (v < 0.0f || v + u > 1.0f) return false;
+  float tt = dot(ac, qv) * inv;
+  if (tt < tmin || tt > tmax) return false;
+  t = tt;
+  return true;
+}
+V xf(const float* m, V p, float w) {  // c0.xyz c1.xyz c2.xyz c3.xyz
+  return {((m[0] * p.x + m[3] * p.y) + m[6] * p.z) + m[9] * w, ((m[1] * p.x + m[4] * p.y) + m[7] * p.z) + m[10] * w,
+          ((m[2] * p.x + m[5] * p.y) + m[8] * p.z) + m[11] * w};
+}
+
+struct Result {
+  uint32_t prim, container;
+  float t;
+};
+const float kTmin = 0.001f;
+
+// plain stream (layout.h): exact box tests
+Result walk_plain(const HostScene& s, V o, V d, Stats* st = nullptr) {
+  const uint32_t* w = s.slots.data();
+  Ray wr = make_ray(o, d, s.early_ok), r = wr;
+  uint32_t i = s.world_begin, ret = ~0u, hit_ret = ~0u;
+  float best = INFINITY;
+  uint32_t prim = 0;
+  for (;;) {
+    const uint32_t* a = w + 4 * (size_t)i;
+    const uint32_t k = a[7];
+    if (k & kBoxFlag) {
+      float mn[3] = {f(a[0]), f(a[1]), f(a[2])}, mx[3] = {f(a[3]), f(a[4]), f(a[5])};
+      const bool truth = box_exact(mn, mx, r, kTmin, best);
+      if (st) {
+        st->boxes++;
+        const int dec = early_decide(mn, mx, r, kTmin, best);
+        if (dec < 0) st->undecided++;
+        else if ((dec != 0) != truth) st->wrong++;
+      }
+      i = truth ? (k & ~kBoxFlag) : a[6];
+    } else if (k == KIND_END) {
+      if (ret == ~0u) break;
+      if (ret & 0x80000000u) r = wr;
+      i = ret & 0x7FFFFFFFu;
+      ret = ~0u;
+    } else if (k == KIND_SPHERE) {
+      float t;
+      if (sphere_hit({f(a[0]), f(a[1]), f(a[2])}, f(a[3]), r.o, r.d, kTmin, best, t))
+        best = t, prim = MRT_REF(MRT_REF_SPHERE, a[4]), hit_ret = ret;
+      i += 2;
+    } else if (k == KIND_TRI) {
+      float t;
+      if (tri_hit({f(a[0]), f(a[1]), f(a[2])}, {f(a[3]), f(a[4]), f(a[5])}, {f(a[8]), f(a[9]), f(a[10])}, r.o, r.d,
+                  kTmin, best, t))
+        best = t, prim = MRT_REF(MRT_REF_TRIANGLE, a[6]), hit_ret = ret;
+      i += 3;
+    } else if (k == KIND_INST) {
+      const float* m = &s.inst_inv[12 * (size_t)a[0]];
+      r = make_ray(xf(m, wr.o, 1.0f), xf(m, wr.d, 0.0f), s.early_ok);
+      ret = (i + 2) | 0x80000000u;
+      i = a[1];
+    } else if (k == KIND_MODEL) {
+      ret = i + 2;
+      i = a[1];
+    } else {
+      fprintf(stderr, "plain: unsupported kind %u\n", k);
+      exit(2);
+    }
+  }
+  uint32_t cont = 0;
+  if (hit_ret != ~0u) {
+    const uint32_t rec = (hit_ret & 0x7FFFFFFFu) - 2;
+    cont = MRT_REF((hit_ret & 0x80000000u) ? MRT_REF_INSTANCE : MRT_REF_MODEL, w[4 * (size_t)rec]);
+  }
+  return {prim, cont, best};
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) return 1;
+  const int n = argc > 2 ? atoi(argv[2]) : 20000;
+  mrt_builder* b = nullptr;
+  mrt_builder_new(1, &b);
+  if (mrt_builder_builtin(b, argv[1], 16.0f / 9.0f, argc > 3 ? argv[3] : "tests/golden") != 0) {
+    printf("%s: %s\n", argv[1], mrt_global_last_error());
+    return 1;
+  }
+  mrt_builder_build_bvh(b);
+  mrt_scene_desc d;
+  mrt_camera cam;
+  mrt_builder_desc(b, &d, &cam);
+  HostScene s;
+  std::string err;
+  if (!build_host_scene(d, s, err)) {
+    printf("%s\n", err.c_str());
+    return 1;
+  }
+  std::mt19937 g(7);
+  std::uniform_real_distribution<float> u(0.0f, 1.0f);
+  Stats st;
+  uint64_t hits = 0, fast = 0;
+  const V o{cam.origin[0], cam.origin[1], cam.origin[2]};
+  V cam_d{0, 0, -1};
+  for (int k = 0; k < n; ++k) {
+    V ro, rd;
+    if (k % 2 == 0) {  // camera ray
+      const float s1 = u(g), t1 = u(g);
+      rd = {((cam.lower_left_corner[0] + cam.horizontal[0] * s1) + cam.vertical[0] * t1) - o.x,
+            ((cam.lower_left_corner[1] + cam.horizontal[1] * s1) + cam.vertical[1] * t1) - o.y,
+            ((cam.lower_left_corner[2] + cam.horizontal[2] * s1) + cam.vertical[2] * t1) - o.z};
+      ro = o;
+      cam_d = rd;
+    } else {  // from the first hit of the previous camera ray, random direction (a bounce)
+      const Result h = walk_plain(s, o, cam_d);
+      if (h.prim == 0) continue;
+      ro = {o.x + cam_d.x * h.t, o.y + cam_d.y * h.t, o.z + cam_d.z * h.t};
+      rd = {u(g) * 2 - 1, u(g) * 2 - 1, u(g) * 2 - 1};
+    }
+    fast += make_ray(ro, rd, s.early_ok).fast;
+    hits += walk_plain(s, ro, rd, &st).prim != 0;
+  }
+  printf("%-14s rays %d (early domain %llu) hits %llu  boxes %llu  left to the exact test %.5f  wrong %llu\n", argv[1],
+         n, (unsigned long long)fast, (unsigned long long)hits, (unsigned long long)st.boxes,
+         (double)st.undecided / std::max<uint64_t>(st.boxes, 1), (unsigned long long)st.wrong);
+  mrt_builder_free(b);
+  return st.wrong ? 1 : 0;
+}
