@@ -291,6 +291,37 @@ def test_random_worlds_with_ties(ctx, seed):
     assert np.array_equal(bo, obo) and rel_l2(rgb, orgb) <= RTOL
 
 
+def test_tiny_coordinates_keep_the_early_decision(ctx):
+    """Vertex coordinates like sin(pi) ~ 1e-16 (and a subnormal) lie outside the
+    qfast domain but inside the early slab decision's (path.h make_tray):
+    hits and bounces stay bit-exact and most box tests are still settled
+    early. Before round 2's split one such coordinate sent every box test of
+    the scene to the exact path (mesh_ply: 100% -> 4%)."""
+    rng = np.random.default_rng(5)
+    b, o = massrt.Builder(3), oracle.Scene(3)
+    mb, mo = b.material(massrt.MAT_LAMBERTIAN, b.solid(0.5, 0.5, 0.5)), o.material(1, o.solid(0.5, 0.5, 0.5))
+    tiny = np.array([1.2e-16, -3e-17, 7e-39, -0.0], dtype=np.float32)
+    for _ in range(3000):
+        tri = rng.normal(size=9).astype(np.float32) * 3
+        pick = rng.random(9) < 0.25
+        tri[pick] = rng.choice(tiny, size=int(pick.sum()))
+        b.add_triangle(mb, tri)
+        o.add_triangle(mo, tri)
+    b.build_bvh()
+    o.build_bvh()
+    b.camera(50.0, (8, 6, 9), (0, 0, 0), aspect=ASPECT)
+    o.camera(50.0, (8, 6, 9), (0, 0, 0), aspect=ASPECT)
+    ctx.upload(b)
+    rays = random_rays(30_000, 7, span=4.0)
+    assert np.array_equal(ctx.trace_rays(rays), o.trace_rays(rays))
+    ctx.reset_counters()
+    rgb, bo = ctx.render(40, 30, 0, 2, seed=3, counters=True)
+    orgb, obo = o.render(40, 30, 0, 2, seed=3)
+    assert np.array_equal(bo, obo) and rel_l2(rgb, orgb) <= RTOL
+    c = ctx.counters()
+    assert 0 < c["box_exact"] < 0.3 * c["node_visits"], c
+
+
 def test_errors_are_reported(ctx):
     import ctypes as C
     fresh = massrt.Context(0)
