@@ -326,8 +326,13 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
         bytes_per_seg = (sum(TRACE_BYTES[k] * cnt[k] for k in TRACE_BYTES) / max(cnt["segments"], 1)
                          + TRACE_RAY_BYTES)
         segs = seg_per_sample * (samples_total / world)  # this rank's share of the timed samples
-        bytes_per_launch = bytes_per_seg * segs / ks["trace_launches"]
-        avg_ms = ks["trace_ms"] / ks["trace_launches"]
+        # traversal launches: k_trace, plus the drain hand-off's fused k_render
+        # launches (render.hip launch_finish_v), which trace the last paths'
+        # segments — their shading time counts too (conservative)
+        fin_ms, fin_n = ks.get("finish_ms", 0.0), int(ks.get("finish_launches", 0))
+        trav_launches = ks["trace_launches"] + fin_n
+        bytes_per_launch = bytes_per_seg * segs / trav_launches
+        avg_ms = (ks["trace_ms"] + fin_ms) / trav_launches
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         stamp = {"scene": scene, "width": W, "height": H, "spp_per_step": spp, "src": src_hash()}
         pmc_path = Path(a.pmc_json) if (a.pmc_json and scene == a.scene) else REPO / "profiles" / f"pmc_{scene}.json"
@@ -348,8 +353,11 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
                      "frac": round(lim["hbm"], 4)} if "hbm" in lim else None),
             "limiter": {k: round(v, 4) for k, v in lim.items()} or None,
             "pmc": str(pmc_path.relative_to(REPO)) + f" (src {stamp['src']})" if pj else None,
-            "kernel": "k_trace", "bytes_per_launch": round(bytes_per_launch),
-            "avg_launch_ms": round(avg_ms, 4), "launches": int(ks["trace_launches"]),
+            "kernel": "k_trace + drain k_render<adopt>", "bytes_per_launch": round(bytes_per_launch),
+            "avg_launch_ms": round(avg_ms, 4), "launches": int(trav_launches),
+            "k_trace": {"launches": int(ks["trace_launches"]),
+                        "avg_launch_ms": round(ks["trace_ms"] / ks["trace_launches"], 4)},
+            "finish": ({"launches": fin_n, "avg_launch_ms": round(fin_ms / fin_n, 4)} if fin_n else None),
             "achieved_per_step": round(bytes_per_seg * segs / elapsed / 1e9, 1),
             "bytes_per_segment": round(bytes_per_seg, 1), "segments_per_sample": round(seg_per_sample, 4),
             "lane_utilisation": round(cnt["lane_steps"] / max(cnt["wave_slots"], 1), 4),

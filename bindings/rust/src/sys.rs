@@ -272,6 +272,8 @@ pub struct mrt_kernel_stats {
     pub trace_launches: u64,
     pub shade_launches: u64,
     pub iterations: u64,
+    pub finish_ms: f64,
+    pub finish_launches: u64,
 }
 
 /// Opaque handles.

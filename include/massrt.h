@@ -260,6 +260,10 @@ typedef struct {
 typedef struct {
   double trace_ms, shade_ms, other_ms;
   uint64_t trace_launches, shade_launches, iterations;
+  /* the drain hand-off: fused k_render launches that finished a queue's last
+   * paths (trace + shade of every remaining bounce; ABI v6) */
+  double finish_ms;
+  uint64_t finish_launches;
 } mrt_kernel_stats;
 
 typedef struct mrt_ctx mrt_ctx;

@@ -469,11 +469,22 @@ __global__ __launch_bounds__(kBlock, MRT_SHADE_WPE) void k_shade(DevScene S, Dev
 // idle lanes take new work items from ctrl->next_work. slot_ro/slot_rd hold
 // each lane's current world ray (re-read when leaving an instance and when
 // shading, instead of keeping it in registers).
-template <bool COUNT, bool ALPHA>
+//
+// ADOPT (the wavefront loop's drain, "finish"): instead of new work items the
+// lanes adopt the paths of a wavefront pool (`pool`, ctrl->active[cur] of
+// them, handed out by ctrl->next_work) in the state k_shade left them — the
+// next ray to trace, T, L, bounces, RNG — and run each to its end. The
+// wavefront loop switches to it once its work counter is exhausted and few
+// paths remain: every per-bounce k_trace launch lasts at least as long as its
+// slowest ray (mesh_ply: ~2 ms), so a pool draining over ~50 bounces pays that
+// floor ~50 times, while here a lane moves on to its path's next segment as
+// soon as its own segment ends.
+template <bool COUNT, bool ALPHA, bool ADOPT>
 __global__ __launch_bounds__(kBlock) void k_render(DevScene S, DevCamera cam, RenderParams rp, float4* slot_ro,
                                                    float4* slot_rd, Ctrl* ctrl, float4* results, DevCounters* cnt,
-                                                   TraceTune tune) {
+                                                   TraceTune tune, PathBufs pool, uint32_t cur) {
   const uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t n_src = ADOPT ? ctrl->active[cur] : rp.G;  // uniform
   const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), S.world_begin, slot_ro, slot_rd, kTmin};
   LocalCounters lc;
   uint32_t seg = 0, nh = 0, nsamples = 0, nbounces = 0;
@@ -491,17 +502,28 @@ __global__ __launch_bounds__(kBlock) void k_render(DevScene S, DevCamera cam, Re
       uint32_t b = 0;
       if (lane_id() == 0) b = atomicAdd(&ctrl->next_work, n_idle);
       b = __shfl(b, 0, 64);
-      drained = b + n_idle >= rp.G;
+      drained = b + n_idle >= n_src;
       if (g == kIdle) {
         const uint32_t w = b + lane_rank(idle);
-        if (w < rp.G) {
+        if (w < n_src) {
           float4 ro, rd;
           uint4 rs;
-          gen_work(cam, rp, w, ro, rd, rs);
-          g = w;
-          k = 0;
-          T = V3{1.0f, 1.0f, 1.0f};
-          L = V3{0.0f, 0.0f, 0.0f};
+          if (ADOPT) {  // a wavefront path: {o, g} {d, bounces} T L rng (PathBufs)
+            ro = pool.ro[w];
+            rd = pool.rd[w];
+            const float4 tv = pool.thr[w], lv = pool.rad[w];
+            rs = pool.rng[w];
+            g = __float_as_uint(ro.w);
+            k = __float_as_uint(rd.w);
+            T = V3{tv.x, tv.y, tv.z};
+            L = V3{lv.x, lv.y, lv.z};
+          } else {
+            gen_work(cam, rp, w, ro, rd, rs);
+            g = w;
+            k = 0;
+            T = V3{1.0f, 1.0f, 1.0f};
+            L = V3{0.0f, 0.0f, 0.0f};
+          }
           rng = PathRng{(unsigned long long)rs.x | ((unsigned long long)rs.y << 32),
                         (unsigned long long)rs.z | ((unsigned long long)rs.w << 32)};
           slot_ro[slot] = ro;
@@ -918,6 +940,11 @@ struct mrt_ctx {
   // 1024/78 KB were 1% and 1-4% slower than no treelet.
   int trace_block = 256;           // k_trace workgroup size with a treelet (MRT_TRACE_BLOCK: 256, 512 or 1024)
   uint32_t treelet_kb = 0;         // treelet budget per workgroup (MRT_TREELET_KB; 0 = none)
+  // a queue whose work is exhausted hands its last <= finish_paths paths to
+  // one fused k_render launch (adopt mode) instead of per-bounce launches
+  // (MRT_FINISH_PATHS; 0 = never). 500k measured best (profiles/r2_experiments/
+  // finish_sweep.txt): mesh_ply 545 -> 678, sphere_grid 638 -> 642 Msamples/s
+  uint32_t finish_paths = 500000;
 
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t*, uint32_t>> pixlists;
   // host-buffer render staging
@@ -1140,15 +1167,37 @@ std::pair<uint32_t*, uint32_t> pixlist(mrt_ctx* c, uint32_t W, uint32_t H, uint3
 
 template <bool ALPHA>
 void launch_render_v(mrt_ctx* c, hipStream_t st, const RenderParams& rp, bool count) {
-  const void* f = count ? (const void*)k_render<true, ALPHA> : (const void*)k_render<false, ALPHA>;
+  const void* f = count ? (const void*)k_render<true, ALPHA, false> : (const void*)k_render<false, ALPHA, false>;
   const uint32_t grid = persistent_grid(c, f, 0);
   ensure_slots(c, (size_t)grid * kBlock);
+  const PathBufs none{};
   if (count)
-    hipLaunchKernelGGL((k_render<true, ALPHA>), dim3(grid), dim3(kBlock), 0, st, c->S, c->cam, rp, c->slot_ro,
-                       c->slot_rd, c->q[0].ctrl, c->results, c->d_cnt, c->tune);
+    hipLaunchKernelGGL((k_render<true, ALPHA, false>), dim3(grid), dim3(kBlock), 0, st, c->S, c->cam, rp, c->slot_ro,
+                       c->slot_rd, c->q[0].ctrl, c->results, c->d_cnt, c->tune, none, 0u);
   else
-    hipLaunchKernelGGL((k_render<false, ALPHA>), dim3(grid), dim3(kBlock), 0, st, c->S, c->cam, rp, c->slot_ro,
-                       c->slot_rd, c->q[0].ctrl, c->results, c->d_cnt, c->tune);
+    hipLaunchKernelGGL((k_render<false, ALPHA, false>), dim3(grid), dim3(kBlock), 0, st, c->S, c->cam, rp, c->slot_ro,
+                       c->slot_rd, c->q[0].ctrl, c->results, c->d_cnt, c->tune, none, 0u);
+  HIP_CHECK(hipGetLastError());
+}
+
+// Finish queue qi's pool bufs[cur] (ctrl->active[cur] paths) with the fused
+// kernel in adopt mode; each queue uses its own range of lane-ray slots.
+template <bool ALPHA>
+void launch_finish_v(mrt_ctx* c, int qi, uint32_t cur, const RenderParams& rp, bool count) {
+  Queue& q = c->q[qi];
+  const void* f = count ? (const void*)k_render<true, ALPHA, true> : (const void*)k_render<false, ALPHA, true>;
+  const uint32_t grid = persistent_grid(c, f, 0, c->n_queues > 1);
+  const size_t lanes = (size_t)grid * kBlock;
+  ensure_slots(c, lanes * kMaxQueues);
+  float4* sro = c->slot_ro + lanes * qi;
+  float4* srd = c->slot_rd + lanes * qi;
+  HIP_CHECK(hipMemsetAsync(&q.ctrl->next_work, 0, 4, q.stream));
+  if (count)
+    hipLaunchKernelGGL((k_render<true, ALPHA, true>), dim3(grid), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, sro, srd,
+                       q.ctrl, c->results, c->d_cnt, c->tune, q.bufs[cur], cur);
+  else
+    hipLaunchKernelGGL((k_render<false, ALPHA, true>), dim3(grid), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, sro,
+                       srd, q.ctrl, c->results, c->d_cnt, c->tune, q.bufs[cur], cur);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1225,6 +1274,17 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
   ensure_results(c, (size_t)n_pix * spp_chunk);
   const int K = c->n_queues;
   const bool timing = (a->flags & MRT_RENDER_TIME_KERNELS) != 0;
+  // the drain hand-off (launch_finish_v): the fused kernel has no traversal
+  // draws or composite surfaces; its lane-ray slots are allocated here, before
+  // any queue runs (ensure_slots reallocates)
+  const bool can_finish = !c->scene_rng && !c->scene_ext && !(a->flags & MRT_RENDER_SIMPLE_TRACE);
+  const uint32_t finish_paths = can_finish ? c->finish_paths : 0u;
+  if (finish_paths) {
+    const void* f = c->scene_alpha ? (count ? (const void*)k_render<true, true, true> : (const void*)k_render<false, true, true>)
+                                   : (count ? (const void*)k_render<true, false, true> : (const void*)k_render<false, false, true>);
+    wait_queues(c, st);
+    ensure_slots(c, (size_t)persistent_grid(c, f, 0, K > 1) * kBlock * kMaxQueues);
+  }
   auto next_event = [&]() {
     if (c->ev_used == c->ev_pool.size()) {
       hipEvent_t e;
@@ -1269,6 +1329,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
     }
     const uint32_t grid = (uint32_t)((c->q[0].cap + kBlock - 1) / kBlock);
     std::vector<std::array<hipEvent_t, 3>> marks;
+    std::vector<std::array<hipEvent_t, 2>> fin_marks;
     const int kBatch = 4;  // even: a status read sees the live pool in active[0]
     struct Loop {
       uint32_t it = 0;
@@ -1321,7 +1382,25 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
         if (L.pending) {  // the previous batch's status (one batch stays in flight)
           HIP_CHECK(hipEventSynchronize(q.ev[L.slot ^ 1]));
           const Ctrl& s = q.h_status[L.slot ^ 1];
-          if (s.active[0] == 0 && q.h_work[L.slot ^ 1] >= rp.G) {
+          if (q.h_work[L.slot ^ 1] >= rp.G && s.active[0] <= finish_paths) {
+            // no new work: the paths left (at most as many as that status
+            // showed) finish in one fused launch after the batch just queued
+            if (s.active[0] > 0) {
+              std::array<hipEvent_t, 2> fm{};
+              if (timing) {
+                fm[0] = next_event();
+                HIP_CHECK(hipEventRecord(fm[0], q.stream));
+              }
+              if (c->scene_alpha)
+                launch_finish_v<true>(c, k, L.it & 1, rp, count);
+              else
+                launch_finish_v<false>(c, k, L.it & 1, rp, count);
+              if (timing) {
+                fm[1] = next_event();
+                HIP_CHECK(hipEventRecord(fm[1], q.stream));
+                fin_marks.push_back(fm);
+              }
+            }
             L.finished = true;
             --open;
           }
@@ -1347,6 +1426,12 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
         c->kstats.trace_launches++;
         c->kstats.shade_launches++;
         c->kstats.iterations++;
+      }
+      for (auto& m : fin_marks) {
+        float t = 0;
+        HIP_CHECK(hipEventElapsedTime(&t, m[0], m[1]));
+        c->kstats.finish_ms += t;
+        c->kstats.finish_launches++;
       }
       c->ev_used = 0;
     }
@@ -1406,6 +1491,7 @@ int mrt_create(int device, mrt_ctx** out) {
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     c->cus = std::max(1, cus);
     c->trace_grid = (uint32_t)c->cus * 4;  // k_trace_simple (debug)
+    if (const char* e = getenv("MRT_FINISH_PATHS")) c->finish_paths = (uint32_t)std::max(0L, atol(e));
     if (getenv("MRT_TRACE_REFILL") || getenv("MRT_TRACE_BOX_MIN")) c->tune_auto_loop = false;
     if (const char* e = getenv("MRT_TRACE_REFILL")) c->tune.refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_PRIM_BATCH")) c->tune.prim_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));

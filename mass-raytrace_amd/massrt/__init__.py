@@ -140,7 +140,8 @@ COUNTER_FIELDS = ["samples", "segments", "node_visits", "sphere_tests", "triangl
 
 class MrtKernelStats(C.Structure):
     _fields_ = [("trace_ms", C.c_double), ("shade_ms", C.c_double), ("other_ms", C.c_double),
-                ("trace_launches", C.c_uint64), ("shade_launches", C.c_uint64), ("iterations", C.c_uint64)]
+                ("trace_launches", C.c_uint64), ("shade_launches", C.c_uint64), ("iterations", C.c_uint64),
+                ("finish_ms", C.c_double), ("finish_launches", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {f: getattr(self, f) for f, _ in self._fields_}

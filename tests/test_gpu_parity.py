@@ -322,6 +322,29 @@ def test_tiny_coordinates_keep_the_early_decision(ctx):
     assert 0 < c["box_exact"] < 0.3 * c["node_visits"], c
 
 
+@pytest.mark.parametrize("scene", ["sphere_grid", "cube_field"])
+def test_drain_handoff_is_bit_identical(small_scenes, monkeypatch, scene):
+    """A queue whose work is exhausted hands its last paths to the fused
+    kernel in adopt mode (render.hip launch_finish_v): the image must be
+    the per-bounce wavefront's bit for bit — never, at once, by default."""
+    b, _ = small_scenes[scene]
+    out = []
+    for v in ("0", "1000000000", None):
+        if v is None:
+            monkeypatch.delenv("MRT_FINISH_PATHS", raising=False)
+        else:
+            monkeypatch.setenv("MRT_FINISH_PATHS", v)
+        c = massrt.Context(0)
+        c.upload(b)
+        c.reset_kernel_stats()
+        out.append(c.render(64, 36, 0, 16, seed=11, flags=massrt.RENDER_TIME_KERNELS))
+        if v == "1000000000":
+            assert c.kernel_stats()["finish_launches"] > 0
+        c.close()
+    for rgb, bo in out[1:]:
+        assert np.array_equal(out[0][0].view(np.uint32), rgb.view(np.uint32)) and np.array_equal(out[0][1], bo)
+
+
 def test_errors_are_reported(ctx):
     import ctypes as C
     fresh = massrt.Context(0)
