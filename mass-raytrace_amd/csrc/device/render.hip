@@ -911,6 +911,21 @@ struct mrt_ctx {
   hipEvent_t fork = nullptr;
   float4* results = nullptr;
   size_t results_cap = 0;
+  // Queue sets (round 2): consecutive render chunks alternate between two
+  // sets of n_queues queues, each with its own work counter (word 32*s of
+  // `work`) and results slab (results_s[s]); a chunk returns to the caller as
+  // soon as every queue of its set has handed its drain to a finish launch,
+  // so the next chunk's paths start while those drains run. acc_done[s]:
+  // recorded on the caller's stream after the accumulate that read slab s.
+  int n_sets = 1;  // MRT_QUEUE_SETS=2: two sets (when 2 * n_queues <= kMaxQueues)
+  int set_next = 0;
+  float4* results_s[2] = {nullptr, nullptr};
+  hipEvent_t acc_done[2] = {nullptr, nullptr};
+  hipEvent_t set_fork[2] = {nullptr, nullptr};
+  // kernel-timing marks resolved lazily (mrt_get_kernel_stats): a timed
+  // render does not wait for its set's drain
+  std::vector<std::array<hipEvent_t, 3>> pend_marks;
+  std::vector<std::array<hipEvent_t, 2>> pend_fin;
   DevCounters* d_cnt = nullptr;
   uint32_t* dbg = nullptr;  // MRT_DEBUG_BOUNDS record (4 words)
   uint32_t trace_grid = 1024;  // k_trace_simple workgroups
@@ -945,6 +960,7 @@ struct mrt_ctx {
   // (MRT_FINISH_PATHS; 0 = never). 500k measured best (profiles/r2_experiments/
   // finish_sweep.txt): mesh_ply 545 -> 678, sphere_grid 638 -> 642 Msamples/s
   uint32_t finish_paths = 500000;
+  uint32_t finish_grid_div = 1;  // the finish launch takes 1/div of its occupancy grid (MRT_FINISH_GRID_DIV)
 
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t*, uint32_t>> pixlists;
   // host-buffer render staging
@@ -1085,22 +1101,24 @@ void launch_trace(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in
   HIP_CHECK(hipGetLastError());
 }
 
+// P paths per queue set (n_queues queues), allocated for every set.
 void ensure_pool(mrt_ctx* c, size_t P) {
   if (P <= c->pool_cap) return;
+  HIP_CHECK(hipDeviceSynchronize());  // a set may still be draining into the old pool
   if (c->pool_mem) HIP_CHECK(hipFree(c->pool_mem));
   c->pool_mem = nullptr;
   c->pool_cap = 0;
   const int K = c->n_queues;
   const size_t per_q = (P + K - 1) / K;
   const size_t per = 16 * (2 * 5 + 1);  // two state sets + hits
-  HIP_CHECK(hipMalloc(&c->pool_mem, (per * per_q + 4096) * K));
+  HIP_CHECK(hipMalloc(&c->pool_mem, (per * per_q + 4096) * K * c->n_sets));
   char* p = (char*)c->pool_mem;
   auto take = [&](size_t bytes) {
     char* r = p;
     p += (bytes + 255) & ~(size_t)255;
     return r;
   };
-  for (int k = 0; k < K; ++k) {
+  for (int k = 0; k < K * c->n_sets; ++k) {
     Queue& q = c->q[k];
     for (int b = 0; b < 2; ++b) {
       q.bufs[b].ro = (float4*)take(16 * per_q);
@@ -1115,16 +1133,22 @@ void ensure_pool(mrt_ctx* c, size_t P) {
   c->pool_cap = per_q * K;
 }
 
+// n samples per results slab, one slab per queue set (results == results_s[0]).
 void ensure_results(mrt_ctx* c, size_t n) {
   if (n <= c->results_cap) return;
-  if (c->results) HIP_CHECK(hipFree(c->results));
-  c->results = nullptr;
-  HIP_CHECK(hipMalloc(&c->results, 16 * n));
+  HIP_CHECK(hipDeviceSynchronize());  // a set may still write or accumulate the old slabs
+  for (int s = 0; s < 2; ++s) {
+    if (c->results_s[s]) HIP_CHECK(hipFree(c->results_s[s]));
+    c->results_s[s] = nullptr;
+  }
+  for (int s = 0; s < c->n_sets; ++s) HIP_CHECK(hipMalloc(&c->results_s[s], 16 * n));
+  c->results = c->results_s[0];
   c->results_cap = n;
 }
 
 void ensure_slots(mrt_ctx* c, size_t n) {
   if (n <= c->slots_cap) return;
+  if (c->slot_ro) HIP_CHECK(hipDeviceSynchronize());  // a queue set's drain may still use them
   if (c->slot_ro) HIP_CHECK(hipFree(c->slot_ro));
   c->slot_ro = nullptr;
   c->slot_rd = nullptr;
@@ -1183,21 +1207,22 @@ void launch_render_v(mrt_ctx* c, hipStream_t st, const RenderParams& rp, bool co
 // Finish queue qi's pool bufs[cur] (ctrl->active[cur] paths) with the fused
 // kernel in adopt mode; each queue uses its own range of lane-ray slots.
 template <bool ALPHA>
-void launch_finish_v(mrt_ctx* c, int qi, uint32_t cur, const RenderParams& rp, bool count) {
+void launch_finish_v(mrt_ctx* c, int qi, uint32_t cur, const RenderParams& rp, bool count, float4* res) {
   Queue& q = c->q[qi];
   const void* f = count ? (const void*)k_render<true, ALPHA, true> : (const void*)k_render<false, ALPHA, true>;
-  const uint32_t grid = persistent_grid(c, f, 0, c->n_queues > 1);
-  const size_t lanes = (size_t)grid * kBlock;
+  const uint32_t full = persistent_grid(c, f, 0, c->n_queues > 1);
+  const size_t lanes = (size_t)full * kBlock;
+  const uint32_t grid = std::max<uint32_t>(c->cus, full / c->finish_grid_div);
   ensure_slots(c, lanes * kMaxQueues);
   float4* sro = c->slot_ro + lanes * qi;
   float4* srd = c->slot_rd + lanes * qi;
   HIP_CHECK(hipMemsetAsync(&q.ctrl->next_work, 0, 4, q.stream));
   if (count)
     hipLaunchKernelGGL((k_render<true, ALPHA, true>), dim3(grid), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, sro, srd,
-                       q.ctrl, c->results, c->d_cnt, c->tune, q.bufs[cur], cur);
+                       q.ctrl, res, c->d_cnt, c->tune, q.bufs[cur], cur);
   else
     hipLaunchKernelGGL((k_render<false, ALPHA, true>), dim3(grid), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, sro,
-                       srd, q.ctrl, c->results, c->d_cnt, c->tune, q.bufs[cur], cur);
+                       srd, q.ctrl, res, c->d_cnt, c->tune, q.bufs[cur], cur);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1282,7 +1307,6 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
   if (finish_paths) {
     const void* f = c->scene_alpha ? (count ? (const void*)k_render<true, true, true> : (const void*)k_render<false, true, true>)
                                    : (count ? (const void*)k_render<true, false, true> : (const void*)k_render<false, false, true>);
-    wait_queues(c, st);
     ensure_slots(c, (size_t)persistent_grid(c, f, 0, K > 1) * kBlock * kMaxQueues);
   }
   auto next_event = [&]() {
@@ -1309,15 +1333,25 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
       // trace(ray, 0) returns (0, 0) for every sample: nothing to add
       continue;
     }
-    // fork: the queues start after everything already on `st`
+    // queue set s: its queues, work counter and results slab
+    const int s = c->set_next;
+    c->set_next = (c->set_next + 1) % c->n_sets;
+    const int qb = s * K;
+    uint32_t* work = c->work + 32 * s;
+    float4* res = c->results_s[s];
+    // fork: set s starts after the accumulate that last read slab s
+    // (acc_done[s], on the caller's stream) — not after everything on `st`,
+    // which may hold the other set's accumulate still waiting for its drain
+    // (the kernels read nothing else the caller's stream writes)
     const uint32_t n0 = (uint32_t)std::min<size_t>(rp.G, c->pool_cap);
-    HIP_CHECK(hipMemcpyAsync(c->work, &n0, 4, hipMemcpyHostToDevice, st));
-    HIP_CHECK(hipEventRecord(c->fork, st));
+    HIP_CHECK(hipStreamWaitEvent(c->q[qb].stream, c->acc_done[s], 0));
+    HIP_CHECK(hipMemcpyAsync(work, &n0, 4, hipMemcpyHostToDevice, c->q[qb].stream));
+    HIP_CHECK(hipEventRecord(c->set_fork[s], c->q[qb].stream));
     uint32_t base = 0;
     for (int k = 0; k < K; ++k) {
-      Queue& q = c->q[k];
+      Queue& q = c->q[qb + k];
       const uint32_t nk = (uint32_t)(((uint64_t)n0 * (k + 1)) / K) - base;  // <= q.cap
-      HIP_CHECK(hipStreamWaitEvent(q.stream, c->fork, 0));
+      if (k) HIP_CHECK(hipStreamWaitEvent(q.stream, c->set_fork[s], 0));
       Ctrl init{{nk, 0}, 0, 0};
       HIP_CHECK(hipMemcpyAsync(q.ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, q.stream));
       if (nk) {
@@ -1339,7 +1373,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
     int open = K;
     while (open > 0) {
       for (int k = 0; k < K; ++k) {
-        Queue& q = c->q[k];
+        Queue& q = c->q[qb + k];
         Loop& L = st_[k];
         if (L.finished) continue;
         for (int b = 0; b < kBatch; ++b, ++L.it) {
@@ -1367,7 +1401,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
             auto* shade = count ? (c->scene_ext ? k_shade<true, true> : k_shade<true, false>)
                                 : (c->scene_ext ? k_shade<false, true> : k_shade<false, false>);
             hipLaunchKernelGGL(shade, dim3(grid), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, q.bufs[cur],
-                               q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, c->work, c->results, c->d_cnt);
+                               q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, work, res, c->d_cnt);
           }
           HIP_CHECK(hipGetLastError());
           if (timing) {
@@ -1377,7 +1411,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
           }
         }
         HIP_CHECK(hipMemcpyAsync(&q.h_status[L.slot], q.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, q.stream));
-        HIP_CHECK(hipMemcpyAsync(&q.h_work[L.slot], c->work, 4, hipMemcpyDeviceToHost, q.stream));
+        HIP_CHECK(hipMemcpyAsync(&q.h_work[L.slot], work, 4, hipMemcpyDeviceToHost, q.stream));
         HIP_CHECK(hipEventRecord(q.ev[L.slot], q.stream));
         if (L.pending) {  // the previous batch's status (one batch stays in flight)
           HIP_CHECK(hipEventSynchronize(q.ev[L.slot ^ 1]));
@@ -1392,9 +1426,9 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
                 HIP_CHECK(hipEventRecord(fm[0], q.stream));
               }
               if (c->scene_alpha)
-                launch_finish_v<true>(c, k, L.it & 1, rp, count);
+                launch_finish_v<true>(c, qb + k, L.it & 1, rp, count, res);
               else
-                launch_finish_v<false>(c, k, L.it & 1, rp, count);
+                launch_finish_v<false>(c, qb + k, L.it & 1, rp, count, res);
               if (timing) {
                 fm[1] = next_event();
                 HIP_CHECK(hipEventRecord(fm[1], q.stream));
@@ -1410,35 +1444,49 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
         if (L.it > 64u * 1024u) throw ApiError{MRT_ERR_HIP, "render did not converge"};
       }
     }
-    // join: `st` continues after every queue
+    // join: `st` continues after every queue of the set (which may still be
+    // running its drain: the host does not wait, the next chunk takes the
+    // other set)
     for (int k = 0; k < K; ++k) {
-      HIP_CHECK(hipEventRecord(c->q[k].join, c->q[k].stream));
-      HIP_CHECK(hipStreamWaitEvent(st, c->q[k].join, 0));
+      HIP_CHECK(hipEventRecord(c->q[qb + k].join, c->q[qb + k].stream));
+      HIP_CHECK(hipStreamWaitEvent(st, c->q[qb + k].join, 0));
     }
-    if (timing) {
-      for (int k = 0; k < K; ++k) HIP_CHECK(hipStreamSynchronize(c->q[k].stream));
-      for (auto& m : marks) {
-        float t0 = 0, t1 = 0;
-        HIP_CHECK(hipEventElapsedTime(&t0, m[0], m[1]));
-        HIP_CHECK(hipEventElapsedTime(&t1, m[1], m[2]));
-        c->kstats.trace_ms += t0;
-        c->kstats.shade_ms += t1;
-        c->kstats.trace_launches++;
-        c->kstats.shade_launches++;
-        c->kstats.iterations++;
-      }
-      for (auto& m : fin_marks) {
-        float t = 0;
-        HIP_CHECK(hipEventElapsedTime(&t, m[0], m[1]));
-        c->kstats.finish_ms += t;
-        c->kstats.finish_launches++;
-      }
-      c->ev_used = 0;
+    if (timing) {  // resolved by mrt_get_kernel_stats (resolve_kernel_timing)
+      c->pend_marks.insert(c->pend_marks.end(), marks.begin(), marks.end());
+      c->pend_fin.insert(c->pend_fin.end(), fin_marks.begin(), fin_marks.end());
     }
-    hipLaunchKernelGGL(k_accumulate, dim3((n_pix + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
-                       (const float4*)c->results, n_pix, cs, (const uint32_t*)pl.first, d_rgb, d_b);
+    hipLaunchKernelGGL(k_accumulate, dim3((n_pix + kBlock - 1) / kBlock), dim3(kBlock), 0, st, (const float4*)res,
+                       n_pix, cs, (const uint32_t*)pl.first, d_rgb, d_b);
     HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipEventRecord(c->acc_done[s], st));  // slab s is free again after this
   }
+}
+
+// Kernel timing of renders flagged MRT_RENDER_TIME_KERNELS, resolved when the
+// stats are read (a timed render does not wait for its queue set's drain).
+void resolve_kernel_timing(mrt_ctx* c) {
+  if (c->pend_marks.empty() && c->pend_fin.empty()) return;
+  for (auto& m : c->pend_marks) {
+    float t0 = 0, t1 = 0;
+    HIP_CHECK(hipEventSynchronize(m[2]));
+    HIP_CHECK(hipEventElapsedTime(&t0, m[0], m[1]));
+    HIP_CHECK(hipEventElapsedTime(&t1, m[1], m[2]));
+    c->kstats.trace_ms += t0;
+    c->kstats.shade_ms += t1;
+    c->kstats.trace_launches++;
+    c->kstats.shade_launches++;
+    c->kstats.iterations++;
+  }
+  for (auto& m : c->pend_fin) {
+    float t = 0;
+    HIP_CHECK(hipEventSynchronize(m[1]));
+    HIP_CHECK(hipEventElapsedTime(&t, m[0], m[1]));
+    c->kstats.finish_ms += t;
+    c->kstats.finish_launches++;
+  }
+  c->pend_marks.clear();
+  c->pend_fin.clear();
+  c->ev_used = 0;
 }
 
 }  // namespace
@@ -1480,7 +1528,17 @@ int mrt_create(int device, mrt_ctx** out) {
       HIP_CHECK(hipEventCreateWithFlags(&q.join, hipEventDisableTiming));
     }
     HIP_CHECK(hipMalloc(&c->work, 256));
+    HIP_CHECK(hipMemset(c->work, 0, 256));
     HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
+    // one queue set unless MRT_QUEUE_SETS=2 (and both sets fit in kMaxQueues):
+    // two sets let a chunk's drain overlap the next chunk, but measured 5-12%
+    // slower (profiles/r2_experiments/queue_sets.txt)
+    if (const char* e = getenv("MRT_QUEUE_SETS"))
+      c->n_sets = (atoi(e) >= 2 && 2 * c->n_queues <= kMaxQueues) ? 2 : 1;
+    for (int s = 0; s < 2; ++s) {
+      HIP_CHECK(hipEventCreateWithFlags(&c->acc_done[s], hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&c->set_fork[s], hipEventDisableTiming));
+    }
     HIP_CHECK(hipMalloc(&c->d_cnt, sizeof(DevCounters)));
     HIP_CHECK(hipMemset(c->d_cnt, 0, sizeof(DevCounters)));
     HIP_CHECK(hipMalloc(&c->dbg, 16));
@@ -1492,6 +1550,7 @@ int mrt_create(int device, mrt_ctx** out) {
     c->cus = std::max(1, cus);
     c->trace_grid = (uint32_t)c->cus * 4;  // k_trace_simple (debug)
     if (const char* e = getenv("MRT_FINISH_PATHS")) c->finish_paths = (uint32_t)std::max(0L, atol(e));
+    if (const char* e = getenv("MRT_FINISH_GRID_DIV")) c->finish_grid_div = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (getenv("MRT_TRACE_REFILL") || getenv("MRT_TRACE_BOX_MIN")) c->tune_auto_loop = false;
     if (const char* e = getenv("MRT_TRACE_REFILL")) c->tune.refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_PRIM_BATCH")) c->tune.prim_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
@@ -1528,7 +1587,11 @@ int mrt_destroy(mrt_ctx* c) {
     if (q.stream) hipStreamSynchronize(q.stream);
   hipFree(c->scene_mem);
   hipFree(c->pool_mem);
-  hipFree(c->results);
+  for (int s = 0; s < 2; ++s) {
+    hipFree(c->results_s[s]);
+    if (c->acc_done[s]) hipEventDestroy(c->acc_done[s]);
+    if (c->set_fork[s]) hipEventDestroy(c->set_fork[s]);
+  }
   hipFree(c->work);
   hipFree(c->gamma_d);
   for (Queue& q : c->q) {
@@ -1788,12 +1851,16 @@ int mrt_get_counters(mrt_ctx* c, mrt_counters* out) {
 int mrt_get_kernel_stats(mrt_ctx* c, mrt_kernel_stats* out) {
   return guarded(c, [&] {
     if (!out) throw ApiError{MRT_ERR_INVALID, "null output"};
+    resolve_kernel_timing(c);
     *out = c->kstats;
   });
 }
 
 int mrt_reset_kernel_stats(mrt_ctx* c) {
-  return guarded(c, [&] { c->kstats = mrt_kernel_stats{}; });
+  return guarded(c, [&] {
+    resolve_kernel_timing(c);
+    c->kstats = mrt_kernel_stats{};
+  });
 }
 
 int mrt_selftest_division(mrt_ctx* c, uint64_t n, uint64_t seed, uint64_t* mismatches) {
