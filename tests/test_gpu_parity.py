@@ -345,6 +345,30 @@ def test_drain_handoff_is_bit_identical(small_scenes, monkeypatch, scene):
         assert np.array_equal(out[0][0].view(np.uint32), rgb.view(np.uint32)) and np.array_equal(out[0][1], bo)
 
 
+def test_queue_sets_option_is_bit_identical(small_scenes, monkeypatch):
+    """MRT_QUEUE_SETS=2: consecutive render calls alternate between two queue
+    sets (pools, work counters, result slabs) and a call returns while its
+    set may still drain; accumulation order into the caller's buffer, hence
+    the image, must not change."""
+    b, _ = small_scenes["sphere_grid"]
+    W, H = 64, 36
+    monkeypatch.delenv("MRT_QUEUE_SETS", raising=False)
+    c = massrt.Context(0)
+    c.upload(b)
+    ref = c.render(W, H, 0, 12, seed=13)
+    c.close()
+    monkeypatch.setenv("MRT_QUEUE_SETS", "2")
+    c = massrt.Context(0)
+    c.upload(b)
+    acc = (np.zeros(W * H * 3, np.float32), np.zeros(W * H, np.uint32))
+    for s0 in (0, 4, 8):
+        acc = c.render(W, H, s0, 4, seed=13, accum=acc)
+    whole = c.render(W, H, 0, 12, seed=13)
+    c.close()
+    for rgb, bo in (acc, whole):
+        assert np.array_equal(ref[0].view(np.uint32), rgb.view(np.uint32)) and np.array_equal(ref[1], bo)
+
+
 def test_errors_are_reported(ctx):
     import ctypes as C
     fresh = massrt.Context(0)
