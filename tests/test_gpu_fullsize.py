@@ -1,4 +1,5 @@
-"""Full-size properties at BASELINE config 2 (SphereGrid 1920x1080): a sampled
+"""Full-size properties at BASELINE config 2 (SphereGrid 1920x1080), configs 3-4
+(cube_field, mesh_ply, mesh_obj at 1080p) and config 5 (4K): a sampled
 pixel subset against the oracle (paths are per-(pixel, sample) independent,
 so the oracle recomputes any subset exactly), determinism, shard additivity."""
 import numpy as np
@@ -29,6 +30,27 @@ def test_fullsize_pixel_subset_matches_oracle(ctx, grid):
     a = rgb.reshape(-1, 3)[px].astype(np.float64)
     assert np.linalg.norm(a - orgb.reshape(-1, 3)) / np.linalg.norm(orgb) <= 1e-4
     assert 1.0 < bo.mean() / spp < 20.0
+
+
+@pytest.mark.parametrize("scene", ["cube_field", "mesh_ply", "mesh_obj"])
+def test_fullsize_pixel_subset_other_configs(ctx, golden_dir, assets_dir, scene):
+    """BASELINE configs 3 and 4 at their stated 1920x1080: 16.6M paths per
+    call, so the pools drain through the adopt-mode hand-off and mesh_*
+    (an 82 MB record stream) runs with the large-stream loop thresholds —
+    the paths the bench times. A pixel subset must match the oracle (bounces
+    bit-exact, radiance rel L2 <= 1e-4)."""
+    src = golden_dir if scene == "cube_field" else assets_dir
+    b = massrt.Builder(1).builtin(scene, ASPECT, src)
+    o = oracle.Scene(1).builtin(scene, ASPECT, src)
+    ctx.upload(b)
+    spp = 8
+    rgb, bo = ctx.render(W, H, 0, spp, seed=3)
+    px = np.arange(11, W * H, 1_499, dtype=np.uint32)
+    orgb, obo = o.render_pixels(W, H, px, 0, spp, seed=3)
+    assert np.array_equal(bo[px], obo)
+    a = rgb.reshape(-1, 3)[px].astype(np.float64)
+    assert np.linalg.norm(a - orgb.reshape(-1, 3)) / np.linalg.norm(orgb) <= 1e-4
+    assert bo.sum() > 0
 
 
 def test_fullsize_deterministic_and_shard_additive(ctx, grid):
