@@ -9,6 +9,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <functional>
+#include <unordered_map>
 #include <string>
 
 #include "build.h"
@@ -120,6 +122,34 @@ __global__ __launch_bounds__(kBuildBlock) void k_level_boxes(const uint32_t* lev
   for (int c = 0; c < 3; ++c) nbox[(size_t)c * T + p] = lo[c], nbox[(size_t)(3 + c) * T + p] = hi[c];
 }
 
+// Nodes in preorder from index `base` (World::bvh_new layout): the boxes of
+// k_level_boxes and the children — item refs for 1- and 2-item nodes (the
+// sorted order), node refs otherwise. Written straight into the node array
+// the host copies back (no per-node host pass over randomly ordered items).
+__global__ __launch_bounds__(kBuildBlock) void k_assemble(const NodeRange* nodes, uint32_t T, const float* nbox,
+                                                          const uint32_t* perm, const uint32_t* item_ref,
+                                                          uint32_t base, mrt_node* out) {
+  const uint32_t p = blockIdx.x * kBuildBlock + threadIdx.x;
+  if (p >= T) return;
+  const NodeRange r = nodes[p];
+  mrt_node d;
+  for (int c = 0; c < 3; ++c) d.min[c] = nbox[(size_t)c * T + p], d.max[c] = nbox[(size_t)(3 + c) * T + p];
+  if (r.cnt <= 2) {
+    d.left = item_ref[perm[r.lo]];
+    d.right = r.cnt == 2 ? item_ref[perm[r.lo + 1]] : MRT_REF(MRT_REF_NONE, 0);
+  } else {
+    d.left = MRT_REF(MRT_REF_NODE, base + r.left_p);
+    d.right = MRT_REF(MRT_REF_NODE, base + r.right_p);
+  }
+  out[p] = d;
+}
+
+// the identity item order (on the device: no n*4-byte pageable copy)
+__global__ __launch_bounds__(kBuildBlock) void k_iota(uint32_t* perm, uint32_t n) {
+  const uint32_t i = blockIdx.x * kBuildBlock + threadIdx.x;
+  if (i < n) perm[i] = i;
+}
+
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
@@ -144,48 +174,51 @@ void device_build_tree(int device, const std::vector<Item>& items, mrt::WyRand& 
   const size_t n = items.size();
   if (n == 0) throw Error(MRT_ERR_INVALID, "BvhNode::new over an empty item list (the reference recurses forever)");
   if (n >= (1ull << 31)) throw Error(MRT_ERR_INVALID, "device BVH build: too many items");
-  // ---- host: node ranges in preorder, one axis draw per node (bvh_new order)
-  std::vector<NodeRange> range;
-  std::vector<uint8_t> axis, depth;
-  range.reserve(2 * n), axis.reserve(2 * n), depth.reserve(2 * n);
-  struct Frame {
-    uint32_t lo, cnt, parent;  // parent: preorder index whose right child this is, or ~0
-    uint8_t depth;
+  // ---- host: node ranges level by level (the tree's shape depends on the
+  // item count alone: n >= 3 splits at n/2), numbered in preorder — a node's
+  // left child is p + 1, its right child p + 1 + size(left subtree) — and
+  // one axis draw per node in preorder (bvh_new order, geom.rs:111).
+  std::unordered_map<uint32_t, uint32_t> memo;
+  std::function<uint32_t(uint32_t)> tree_size = [&](uint32_t c) -> uint32_t {
+    if (c <= 2) return 1u;
+    auto it = memo.find(c);
+    if (it != memo.end()) return it->second;
+    const uint32_t v = 1u + tree_size(c / 2) + tree_size(c - c / 2);
+    memo.emplace(c, v);
+    return v;
   };
-  std::vector<Frame> stack{{0, (uint32_t)n, ~0u, 0}};
-  uint32_t max_depth = 0;
-  while (!stack.empty()) {
-    const Frame f = stack.back();
-    stack.pop_back();
-    const uint32_t p = (uint32_t)range.size();
-    if (f.parent != ~0u) range[f.parent].right_p = p;
-    range.push_back(NodeRange{f.lo, f.cnt, ~0u, ~0u});
-    axis.push_back((uint8_t)rng.axis());  // fastrand::u8(0..3), geom.rs:111
-    depth.push_back(f.depth);
-    if (f.depth > max_depth) max_depth = f.depth;
-    if (f.cnt >= 3) {
-      const uint32_t half = f.cnt / 2;
-      range[p].left_p = p + 1;
-      stack.push_back(Frame{f.lo + half, f.cnt - half, p, (uint8_t)(f.depth + 1)});  // right, after the left subtree
-      stack.push_back(Frame{f.lo, half, ~0u, (uint8_t)(f.depth + 1)});
+  const uint32_t T = tree_size((uint32_t)n);
+  std::vector<NodeRange> range(T);
+  std::vector<uint8_t> axis(T);
+  for (uint32_t p = 0; p < T; ++p) axis[p] = (uint8_t)rng.axis();  // fastrand::u8(0..3) per node, in preorder
+  struct Frame {
+    uint32_t p, lo, cnt;
+  };
+  std::vector<std::vector<Seg>> segs;
+  std::vector<uint32_t> level_off{0}, level_nodes;
+  level_nodes.reserve(T);
+  std::vector<Frame> cur{{0u, 0u, (uint32_t)n}}, next;
+  while (!cur.empty()) {  // one tree level, in ascending lo (= ascending preorder index)
+    segs.emplace_back();
+    next.clear();
+    for (const Frame& f : cur) {
+      NodeRange& r = range[f.p];
+      r = NodeRange{f.lo, f.cnt, ~0u, ~0u};
+      level_nodes.push_back(f.p);
+      if (f.cnt >= 2) segs.back().push_back(Seg{f.lo, f.cnt, axis[f.p], 0});
+      if (f.cnt >= 3) {
+        const uint32_t half = f.cnt / 2;
+        r.left_p = f.p + 1;
+        r.right_p = f.p + 1 + tree_size(half);
+        next.push_back(Frame{r.left_p, f.lo, half});
+        next.push_back(Frame{r.right_p, f.lo + half, f.cnt - half});
+      }
     }
+    level_off.push_back((uint32_t)level_nodes.size());
+    std::swap(cur, next);
   }
-  const uint32_t T = (uint32_t)range.size();
-  const uint32_t L = max_depth + 1;
-  // level lists: sort segments (cnt >= 2, ascending lo) and all nodes
-  std::vector<std::vector<Seg>> segs(L);
-  std::vector<uint32_t> level_off(L + 1, 0), level_nodes(T);
-  for (uint32_t p = 0; p < T; ++p) level_off[depth[p] + 1]++;
-  for (uint32_t l = 0; l < L; ++l) level_off[l + 1] += level_off[l];
-  {
-    std::vector<uint32_t> fill(level_off.begin(), level_off.end() - 1);
-    for (uint32_t p = 0; p < T; ++p) {
-      level_nodes[fill[depth[p]]++] = p;
-      if (range[p].cnt >= 2) segs[depth[p]].push_back(Seg{range[p].lo, range[p].cnt, axis[p], 0});
-    }
-  }
-  for (auto& s : segs)  // preorder within a level is already ascending lo; keep it explicit
-    std::sort(s.begin(), s.end(), [](const Seg& a, const Seg& b) { return a.lo < b.lo; });
+  const uint32_t L = (uint32_t)segs.size();
+  if (level_nodes.size() != T) throw Error(MRT_ERR_INVALID, "device BVH build: node count mismatch (internal)");
   const auto t1 = clock::now();
 
   // ---- device
@@ -197,12 +230,12 @@ void device_build_tree(int device, const std::vector<Item>& items, mrt::WyRand& 
     ~StreamGuard() { (void)hipStreamDestroy(s); }
   } sg{st};
   std::vector<float> hb(6 * n);
-  std::vector<uint32_t> perm0(n);
+  std::vector<uint32_t> href(n);
   for (size_t i = 0; i < n; ++i) {
     const BoundingBox& b = items[i].box;
     hb[0 * n + i] = b.minimum.x, hb[1 * n + i] = b.minimum.y, hb[2 * n + i] = b.minimum.z;
     hb[3 * n + i] = b.maximum.x, hb[4 * n + i] = b.maximum.y, hb[5 * n + i] = b.maximum.z;
-    perm0[i] = (uint32_t)i;
+    href[i] = items[i].ref;
   }
   size_t total_segs = 0;
   for (auto& s : segs) total_segs += s.size();
@@ -211,8 +244,12 @@ void device_build_tree(int device, const std::vector<Item>& items, mrt::WyRand& 
   DevBuf<unsigned long long> d_keys(n), d_keys2(n);
   DevBuf<Seg> d_segs(total_segs ? total_segs : 1);
   DevBuf<NodeRange> d_range(T);
+  DevBuf<uint32_t> d_ref(n);
+  DevBuf<mrt_node> d_out(T);
   BUILD_CHECK(hipMemcpyAsync(d_box.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice, st));
-  BUILD_CHECK(hipMemcpyAsync(d_perm.p, perm0.data(), n * 4, hipMemcpyHostToDevice, st));
+  BUILD_CHECK(hipMemcpyAsync(d_ref.p, href.data(), n * 4, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_iota, dim3(grid_for(n)), dim3(kBuildBlock), 0, st, d_perm.p, (uint32_t)n);
+  BUILD_CHECK(hipGetLastError());
   BUILD_CHECK(hipMemcpyAsync(d_range.p, range.data(), (size_t)T * sizeof(NodeRange), hipMemcpyHostToDevice, st));
   BUILD_CHECK(hipMemcpyAsync(d_level_nodes.p, level_nodes.data(), (size_t)T * 4, hipMemcpyHostToDevice, st));
   BUILD_CHECK(hipMemsetAsync(d_nan.p, 0, 4, st));
@@ -247,35 +284,26 @@ void device_build_tree(int device, const std::vector<Item>& items, mrt::WyRand& 
                        cnt, d_range.p, perm, d_box.p, d_box.p + 3 * n, (uint32_t)n, d_nbox.p, T);
     BUILD_CHECK(hipGetLastError());
   }
-  std::vector<float> nb(6 * (size_t)T);
-  std::vector<uint32_t> fperm(n);
+  // ---- nodes in preorder from the first free index (World::bvh_new layout),
+  // assembled on the device and copied straight into the node array
+  const uint32_t base = (uint32_t)nodes.size();
+  hipLaunchKernelGGL(k_assemble, dim3(grid_for(T)), dim3(kBuildBlock), 0, st, d_range.p, T, d_nbox.p, perm, d_ref.p,
+                     base, d_out.p);
+  BUILD_CHECK(hipGetLastError());
   uint32_t nan_flag = 0;
-  BUILD_CHECK(hipMemcpyAsync(nb.data(), d_nbox.p, nb.size() * 4, hipMemcpyDeviceToHost, st));
-  BUILD_CHECK(hipMemcpyAsync(fperm.data(), perm, n * 4, hipMemcpyDeviceToHost, st));
   BUILD_CHECK(hipMemcpyAsync(&nan_flag, d_nan.p, 4, hipMemcpyDeviceToHost, st));
   BUILD_CHECK(hipStreamSynchronize(st));
   if (nan_flag)
     throw Error(MRT_ERR_INVALID, "device BVH build: a NaN bounding-box key (the reference's sort order is undefined)");
-  const auto t2 = clock::now();
-
-  // ---- nodes in preorder from the first free index (World::bvh_new layout)
-  const uint32_t base = (uint32_t)nodes.size();
   nodes.resize(base + (size_t)T);
-  for (uint32_t p = 0; p < T; ++p) {
-    const NodeRange& r = range[p];
-    mrt_node& d = nodes[base + p];
-    for (int c = 0; c < 3; ++c) d.min[c] = nb[(size_t)c * T + p], d.max[c] = nb[(size_t)(3 + c) * T + p];
-    if (r.cnt == 1) {
-      d.left = items[fperm[r.lo]].ref;
-      d.right = MRT_REF(MRT_REF_NONE, 0);
-    } else if (r.cnt == 2) {
-      d.left = items[fperm[r.lo]].ref;
-      d.right = items[fperm[r.lo + 1]].ref;
-    } else {
-      d.left = MRT_REF(MRT_REF_NODE, base + r.left_p);
-      d.right = MRT_REF(MRT_REF_NODE, base + r.right_p);
-    }
+  try {
+    BUILD_CHECK(hipMemcpyAsync(nodes.data() + base, d_out.p, (size_t)T * sizeof(mrt_node), hipMemcpyDeviceToHost, st));
+    BUILD_CHECK(hipStreamSynchronize(st));
+  } catch (...) {
+    nodes.resize(base);  // the node array is unchanged by a failed build
+    throw;
   }
+  const auto t2 = clock::now();
   root_box.minimum = V3{nodes[base].min[0], nodes[base].min[1], nodes[base].min[2]};
   root_box.maximum = V3{nodes[base].max[0], nodes[base].max[1], nodes[base].max[2]};
   if (stats) {
