@@ -196,12 +196,15 @@ struct TRay {
   float yx, yy, yz;
   float oyx, oyy, oyz;  // RN(o.k * y.k)
   // |om| = max(max_k |oy.k| * 2^-20, 2^-120), the early decision's absolute
-  // margin term (box_hit_any); its sign bit set: the exact test may NOT use
-  // qfast (the ray or the scene is outside the qfast domain below)
+  // margin term (box_hit_any), or +inf when the early decision does not apply
+  // to this ray (outside the early domain below: every box test is exact);
+  // its sign bit set: the exact test may NOT use qfast (the ray or the scene
+  // is outside the qfast domain below)
   float om;
-  Recip a;    // |d|^2 for Sphere::intersect
-  bool fast;  // the early slab decision applies to this ray (early domain below)
+  Recip a;  // |d|^2 for Sphere::intersect
 };
+// the early slab decision applies to this ray (early domain below)
+MRT_DEV bool tray_fast(const TRay& r) { return fabsf(r.om) != INFINITY; }
 // qfast domain: with every box coordinate and ray-origin coordinate in
 // {0} U [2^-40, 2^28] (scene bound checked on the host, origin here) each
 // nonzero numerator (min - o) is >= 2^-63 and < 2^29; with |d| in
@@ -238,8 +241,9 @@ MRT_DEV TRay make_tray(V3 o, V3 d, uint32_t scene_flags) {
   r.a = make_recip(length_squared(d));
   const bool dok = dir_ok(d.x) && dir_ok(d.y) && dir_ok(d.z);
   const bool qok = (scene_flags & 1u) && coord_ok(o.x) && coord_ok(o.y) && coord_ok(o.z) && dok;
-  r.om = qok ? om : -om;
-  r.fast = (scene_flags & 2u) && orig_ok(o.x) && orig_ok(o.y) && orig_ok(o.z) && dok;
+  const bool fast = (scene_flags & 2u) && orig_ok(o.x) && orig_ok(o.y) && orig_ok(o.z) && dok;
+  const float m = fast ? om : INFINITY;
+  r.om = qok ? m : -m;
   return r;
 }
 MRT_DEV float qfast(float a, float b, float y) {
@@ -488,7 +492,10 @@ MRT_DEV float slab_margin(const TRay& r, float t0, float t1) {
 }
 template <bool COUNT = false>
 MRT_DEV bool box_hit_any(V3 mn, V3 mx, const TRay& r, float tmin, float tmax, LocalCounters* lc = nullptr) {
-  if (r.fast) {
+  // no branch on the ray's domain: outside the early domain |om| = +inf makes
+  // the margin +inf (or NaN), so neither comparison decides and the exact
+  // test runs
+  {
     float t0, t1;
     slab_fast(mn, mx, r, tmin, tmax, t0, t1);
     const float m = slab_margin(r, t0, t1);

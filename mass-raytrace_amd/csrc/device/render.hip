@@ -848,7 +848,7 @@ __global__ __launch_bounds__(kBlock) void k_selftest_slab(unsigned long long n, 
     for (int k = 0; k < 3; ++k) early = early && orig_ok(mn[k]) && orig_ok(mx[k]);
     if (!early) continue;
     const TRay ray = make_tray(o, d, ok ? 3u : 2u);
-    if (!ray.fast) continue;
+    if (!tray_fast(ray)) continue;
     const uint64_t rt = rnd();
     const float tmin = (rt & 3) == 0 ? nudge(t, -(int)(rt >> 2 & 3)) : 0.001f;
     const float tmax = (rt >> 4 & 3) == 0 ? INFINITY : ((rt >> 4 & 3) == 1 ? nudge(t, (int)(rt >> 6 & 7) - 3) : t * 2.0f);
