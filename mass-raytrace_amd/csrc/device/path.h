@@ -523,6 +523,7 @@ MRT_DEV void trav_fetch(const TravIn& in, Trav& t) {
   if (++t.steps > (1u << 24)) {  // record and stop instead of looping
     MRT_IDX(in.S, 0xFFFFFFF0u, 0u, 5);
     t.done = true;
+    t.s1.w = KIND_END;  // a done lane never holds a box record (k_trace's box run)
     return;
   }
 #endif

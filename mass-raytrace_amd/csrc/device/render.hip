@@ -282,23 +282,25 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(ALPHA == 0 
       // box run: keep stepping boxes with little per-step overhead while at
       // least tune.box_min lanes are at one (lanes reaching a primitive wait)
       for (;;) {
-        const bool at_box = !t[q].done && trav_at_box(t[q]);
-        const unsigned long long bm = __builtin_amdgcn_ballot_w64(at_box);
+        // a done lane holds an END record (or an idle lane's zeros), never a
+        // box, so the record's flag alone decides (no done mask in the ballot)
+        const bool run_box = trav_at_box(t[q]);
+        const unsigned long long bm = __builtin_amdgcn_ballot_w64(run_box);
         if ((uint32_t)__popcll(bm) < tune.box_min) break;
-        if (at_box) trav_box_index<COUNT>(tin, t[q], lc);
-        if (at_box) trav_fetch<LDS>(tin, t[q]);
+        if (run_box) trav_box_index<COUNT>(tin, t[q], lc);
+        if (run_box) trav_fetch<LDS>(tin, t[q]);
 #ifdef MRT_PROBE  // experiment builds: texel_taps = box-run iterations, wave_slots = uniform ones
         if (COUNT) {
-          const uint32_t f = __builtin_amdgcn_readfirstlane(at_box ? t[q].i : 0xFFFFFFFFu);
-          const bool uni = __builtin_amdgcn_ballot_w64(at_box && t[q].i != f) == 0;
+          const uint32_t f = __builtin_amdgcn_readfirstlane(run_box ? t[q].i : 0xFFFFFFFFu);
+          const bool uni = __builtin_amdgcn_ballot_w64(run_box && t[q].i != f) == 0;
           lc.texel_taps += lane_id() == 0 ? 1u : 0u;
           lc.wave_slots += (lane_id() == 0 && uni) ? 1u : 0u;
-          lc.lane_steps += at_box ? 1u : 0u;
+          lc.lane_steps += run_box ? 1u : 0u;
         }
 #else
         if (COUNT) {
           lc.wave_slots += lane_id() == 0 ? 64u : 0u;
-          lc.lane_steps += at_box ? 1u : 0u;
+          lc.lane_steps += run_box ? 1u : 0u;
         }
 #endif
       }
