@@ -44,7 +44,6 @@ all-logical-cores run; host model and core counts are recorded.
 from __future__ import annotations
 
 import argparse
-import hashlib
 import json
 import os
 import sys
@@ -64,7 +63,10 @@ CACHE_PEAK_GBS = 36900.0
 TRACE_BYTES = {"node_visits": 32, "triangle_tests": 36, "sphere_tests": 16, "instance_entries": 48}
 TRACE_RAY_BYTES = 32 + 16  # ray origin+direction read, hit record written
 
-SRC_DIRS = [REPO / "mass-raytrace_amd" / "csrc", REPO / "include"]
+# k_shade's algorithmic bytes per shaded path: the path state
+# read (ro, rd, thr, rad, rng: 5 x 16 B) + its hit record (16 B) and the
+# state written to the next pool (5 x 16 B)
+SHADE_BYTES = 5 * 16 + 16 + 5 * 16
 
 
 def parse():
@@ -88,18 +90,34 @@ def parse():
     ap.add_argument("--fused", action="store_true", help="one persistent k_render instead of the k_trace/k_shade loop")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--pmc-json", default=None, help="PMC summary (default profiles/pmc_<scene>.json)")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in render() call-pattern runs")
+    ap.add_argument("--dropin-batch", type=int, default=64, help="1-spp passes per mrt_image_render call")
     return ap.parse_args()
 
 
 def src_hash() -> str:
-    """Hash of the library sources: a PMC profile is valid only for the code it measured."""
-    h = hashlib.sha256()
-    for d in SRC_DIRS:
-        for p in sorted(d.rglob("*")):
-            if p.is_file() and p.suffix in (".h", ".hip", ".cpp"):
-                h.update(str(p.relative_to(REPO)).encode())
-                h.update(p.read_bytes())
-    return h.hexdigest()[:16]
+    """Hash of the library sources (tools/src_hash.py): a PMC profile is valid
+    only for the code it measured, and the loaded library must carry it."""
+    sys.path.insert(0, str(REPO / "tools"))
+    from src_hash import src_hash as h
+
+    return h()
+
+
+def launch_plan(gpus: int, env: dict, argv: list, port: int):
+    """How `bench.py --gpus N` runs: None = this process is the (only) rank
+    or one rank of a launcher's job; else the command that starts N ranks
+    (torch.distributed.run, one process per GPU, rendezvous on 127.0.0.1).
+    A launcher's WORLD_SIZE must agree with --gpus."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {gpus}: the launcher and the flag disagree")
+        return None
+    if gpus <= 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
 
 
 def asset_dir(scene: str, rank: int = 0, world: int = 1) -> Path:
@@ -176,11 +194,16 @@ def cpu_baseline(scene: str, W: int, H: int, max_depth: int, seconds: float, see
     value = samples / secs / 1e6
     secs_all, rows_all, _, _ = run(logical, n_rows, seed + 9)
     value_all = logical * W * rows_all / secs_all / 1e6
+    quota = host["cgroup_cpu_quota"]
+    cpus_avail = min(host["affinity_cpus"] or logical, int(quota) if quota else logical)
     out = {
         "value": round(value, 4),
         "unit": "Msamples/s",
-        "cores": ref_threads,
+        # the reference's num_cpus-2 threads run on the CPUs this job may use
+        "cores": cpus_avail,
         "threads": ref_threads,
+        "cpus_available": cpus_avail,
+        "host_physical_cores": host["physical_cores"],
         "kind": "port",
         "all_cores": {"value": round(value_all, 4), "threads": logical, "seconds": round(secs_all, 2)},
         "host": host,
@@ -189,7 +212,6 @@ def cpu_baseline(scene: str, W: int, H: int, max_depth: int, seconds: float, see
                    f"in {secs:.1f}s; oracle reference mode (recursive virtual traversal, main.rs:159-290 "
                    f"threading), g++ -O3 scalar"),
     }
-    quota = host["cgroup_cpu_quota"]
     if quota and quota < logical:
         # This job may use only `quota` CPUs of the host, so the runs above are
         # quota-bound. Measure the rate per CPU with exactly that many workers
@@ -234,6 +256,49 @@ def c1_runs(a) -> dict:
                     "threads": threads, "passes_per_thread": spp // threads, "kind": "port"},
             "gpu": {"value": round(W * H * spp / gsecs / 1e6, 2), "unit": "Msamples/s", "seconds": round(gsecs, 4),
                     "note": "one mrt_render call incl. host copies; too small to fill the GPU"}}
+
+
+def dropin_run(a, scene: str, headline: float | None) -> dict:
+    """The drop-in render() call pattern (bindings/rust/src/lib.rs `render`,
+    restated as massrt.render): one frame of the reference's render()
+    (main.rs:150-295) at frame_limit 1 — pre-pass, Image::clear, then
+    num_cpus-2 workers x 1 pass each = that many 1-spp passes (main.rs:159-160,
+    243-280), run --dropin-batch passes per mrt_image_render call into the
+    device-resident image, and after every batch the update the reference's
+    UI gets (UserEvent::Update -> to_rgb_bytes): the display bytes tone-mapped
+    on the GPU and copied to the host. Timed: the whole render() call."""
+    import torch
+
+    import massrt
+
+    W, H = a.width, a.height
+    ctx = massrt.Context(torch.cuda.current_device())
+    b = massrt.Builder(1).builtin(scene, float(massrt.ASPECT_RATIO), str(asset_dir(scene)))
+    ctx.upload(b)
+    b.close()
+    img = massrt.Image(ctx, W, H)
+    workers = massrt.default_workers()
+    st = massrt.SampleStreams(a.seed)
+    last = {}
+
+    def update(im, passes):  # the UI's redraw: display bytes on the host
+        last["bytes"] = im.tonemap()
+        last["passes"] = passes
+
+    massrt.render(img, st, frame_limit=1, workers=min(workers, 2 * a.dropin_batch), batch=a.dropin_batch,
+                  update=update)  # warm-up frame (untimed)
+    t0 = time.perf_counter()
+    n = massrt.render(img, st, frame_limit=1, workers=workers, batch=a.dropin_batch, update=update)
+    secs = time.perf_counter() - t0
+    assert last["passes"] == n == workers
+    img.close()
+    ctx.close()
+    value = W * H * n / secs / 1e6
+    return {"workload": f"{scene} {W}x{H}, render(frame_limit=1): {workers} workers (num_cpus-2) x 1 pass",
+            "value": round(value, 2), "unit": "Msamples/s", "seconds": round(secs, 3), "passes": n,
+            "batch": a.dropin_batch, "updates": -(-n // a.dropin_batch),
+            "of_headline": round(value / headline, 3) if headline else None,
+            "includes": "pre-pass, clear, every batch's render and tonemap + 6 MB device-to-host copy"}
 
 
 def load_pmc(path: Path, stamp: dict):
@@ -298,6 +363,7 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
     torch.cuda.synchronize()
     cnt = ctx.counters()
     ctx.reset_kernel_stats()
+    frame.gather_ms()  # drop the warmup publishes
 
     timing = not a.no_kernel_timing
     if world > 1:
@@ -311,10 +377,16 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    gather_ms = frame.gather_ms()
+    per_rank = None
+    if world > 1:  # every rank's wall time and publish time; the job's time is the slowest rank's
+        t = torch.tensor([elapsed, gather_ms], dtype=torch.float64)
+        if a.dist_backend == "nccl":
+            t = t.to(dev)
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        per_rank = [(float(p[0]), float(p[1])) for p in parts]
+        elapsed = max(e for e, _ in per_rank)
     ks = ctx.kernel_stats()
 
     samples_total = W * H * spp * steps
@@ -365,9 +437,25 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
             "box_exact_frac": round(cnt.get("box_exact", 0) / max(cnt["node_visits"], 1), 5),
         }
 
+    shade = None
+    if timing and cnt.get("shaded") and ks["shade_launches"] > 0:
+        # k_shade: HBM-streaming (path state in and out), SHADE_BYTES per shaded path
+        shaded = cnt["shaded"] / max(cnt["samples"], 1) * (samples_total / world)
+        sb = SHADE_BYTES * shaded / ks["shade_launches"]
+        sms = ks["shade_ms"] / ks["shade_launches"]
+        shade = {"kernel": "k_shade", "bound": "hbm", "bytes_per_launch": round(sb), "avg_launch_ms": round(sms, 4),
+                 "launches": int(ks["shade_launches"]), "achieved": round(sb / (sms * 1e-3) / 1e9, 1),
+                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(sb / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                 "bytes_per_path": SHADE_BYTES, "paths_per_sample": round(cnt["shaded"] / max(cnt["samples"], 1), 4)}
     out = {"scene": scene, "value": round(value, 3), "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps,
            "warmup": warmup, "width": W, "height": H, "spp_per_step": spp, "samples_per_step": W * H * spp,
-           "scene_load_s": round(t_load, 2), "roofline": roof}
+           "scene_load_s": round(t_load, 2), "roofline": roof, "roofline_k_shade": shade}
+    if world > 1:
+        out["gather"] = {"transport": "RCCL (dist.gather over xGMI)" if a.dist_backend == "nccl" else
+                         f"{a.dist_backend} (host-staged)", "bytes_per_rank_per_step": frame.slab_bytes,
+                         "bytes_to_rank0_per_step": W * H * 16, "ms_per_step_rank0": round(per_rank[0][1] / steps, 3),
+                         "per_rank_ms_per_step": [round(e / steps * 1e3, 3) for e, _ in per_rank],
+                         "per_rank_gather_ms_per_step": [round(g / steps, 3) for _, g in per_rank]}
     if rank == 0:
         out["mean_bounces_per_sample"] = round(
             float(frame.frame()[1].double().sum().item()) / (W * H * spp * (steps + max(1, warmup))), 4)
@@ -379,17 +467,38 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
             out["cpu_baseline"] = cpu_baseline(scene, W, H, a.max_depth, a.cpu_seconds, a.seed)
         except Exception as e:  # baseline failure must not hide the GPU number
             out["cpu_baseline"] = {"value": None, "error": str(e)}
-        if out["cpu_baseline"].get("value"):
-            out["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
-        if out["cpu_baseline"].get("host_estimate"):
-            out["gpu_over_cpu_host_estimate"] = round(value / out["cpu_baseline"]["host_estimate"]["value"], 1)
+        cb = out["cpu_baseline"]
+        if cb.get("host_estimate"):
+            # the whole host (every logical CPU; estimated from the quota-bound rate)
+            out["gpu_over_cpu"] = round(value / cb["host_estimate"]["value"], 1)
+            out["gpu_over_cpu_basis"] = "whole host (host_estimate, all logical CPUs)"
+            if cb.get("value"):
+                out[f"gpu_over_cpu_quota{cb['cpus_available']}"] = round(value / cb["value"], 1)
+        elif cb.get("value"):
+            out["gpu_over_cpu"] = round(value / cb["value"], 1)
+            out["gpu_over_cpu_basis"] = f"measured on {cb['cpus_available']} CPUs (the whole host)"
     return out
 
 
 def main():
     a = parse()
+    # --gpus N without a launcher: start the N ranks ourselves, before anything
+    # here touches a GPU, and exit with their status (rank 0 prints the line)
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = launch_plan(a.gpus, os.environ, sys.argv[1:], port)
+    if cmd is not None:
+        import subprocess
+
+        sys.exit(subprocess.call(cmd, env=dict(os.environ)))
+
     import torch
     import torch.distributed as dist
+
+    import massrt
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -407,6 +516,16 @@ def main():
     sec = None
     if a.secondary and a.secondary != "none" and a.secondary != a.scene:
         sec = run_scene(a, a.secondary, a.secondary_steps, 1, rank, world, dev, cpu)
+
+    dropin = None
+    if rank == 0 and world == 1 and not a.no_dropin:
+        dropin = {}
+        for sc, ref in ((a.scene, head["value"]), (a.secondary, sec["value"] if sec else None)):
+            if sc and sc != "none":
+                try:
+                    dropin[sc] = dropin_run(a, sc, ref)
+                except Exception as e:
+                    dropin[sc] = {"error": str(e)}
 
     c1 = None
     if cpu:
@@ -442,11 +561,20 @@ def main():
             "roofline": head["roofline"],
             "cpu_baseline": head.get("cpu_baseline"),
         }
-        for k in ("gpu_over_cpu", "gpu_over_cpu_host_estimate"):
-            if k in head:
-                line["config"][k] = head[k]
+        for k, v in head.items():
+            if k.startswith("gpu_over_cpu"):
+                line["config"][k] = v
         if c1:
             line["config"]["c1"] = c1
+        if dropin:
+            line["config"]["dropin"] = dropin
+        if head.get("roofline_k_shade"):
+            line["roofline_k_shade"] = head["roofline_k_shade"]
+        if head.get("gather"):
+            line["config"]["gather"] = head["gather"]
+        tree = src_hash()
+        line["build"] = {"library": massrt.build_info(), "tree": f"src {tree}",
+                         "match": massrt.build_info() == f"src {tree}"}
         if sec:
             sec["workload"] = f"{sec['scene']} {a.width}x{a.height}x{a.total_spp}spp, max_depth {a.max_depth} " \
                               f"(north_star target: 1M-triangle binary PLY, BASELINE config 4)"

@@ -5,8 +5,9 @@
 //! called by `worker`, main.rs:114-118). With this crate that function keeps its
 //! signature and body shape: the world is flattened once through `SceneSink`
 //! (each reference type implements `Export`), uploaded,
-//! and every pass is one `mrt_render` call whose sums are merged into the
-//! shared `Image` exactly like `Image::merge` (main.rs:629-638).
+//! and `render()` below runs the reference's pass loop over a device-resident
+//! `GpuImage` (one context may span several GPUs), handing the sums and the
+//! pass count to the caller's `Image` after every batch.
 //!
 //! Source only here (no Rust toolchain in the build image); the FFI layout is
 //! checked against include/massrt.h by tests/test_rust_binding.py.
@@ -111,6 +112,26 @@ pub struct Context {
 unsafe impl Send for Context {}
 
 impl Context {
+    /// One context over several devices (mrt_create_multi): each renders its
+    /// share of the frame's tiles; reads gather them.
+    pub fn new_multi(devices: &[i32]) -> Result<Context, MrtError> {
+        let mut raw = std::ptr::null_mut();
+        let rc = unsafe { mrt_create_multi(devices.len() as i32, devices.as_ptr(), &mut raw) };
+        if rc != MRT_OK {
+            let message = unsafe { CStr::from_ptr(mrt_global_last_error()) }.to_string_lossy().into_owned();
+            return Err(MrtError { code: rc, message });
+        }
+        Ok(Context { raw })
+    }
+
+    pub fn devices(&self) -> Result<Vec<i32>, MrtError> {
+        let mut n = 0i32;
+        self.check(unsafe { mrt_context_devices(self.raw, &mut n, std::ptr::null_mut()) })?;
+        let mut ids = vec![0i32; n as usize];
+        self.check(unsafe { mrt_context_devices(self.raw, &mut n, ids.as_mut_ptr()) })?;
+        Ok(ids)
+    }
+
     pub fn new(device: i32) -> Result<Context, MrtError> {
         let mut raw = std::ptr::null_mut();
         let rc = unsafe { mrt_create(device, &mut raw) };
@@ -121,7 +142,7 @@ impl Context {
         Ok(Context { raw })
     }
 
-    fn check(&self, rc: i32) -> Result<(), MrtError> {
+    pub fn check(&self, rc: i32) -> Result<(), MrtError> {
         if rc == MRT_OK {
             return Ok(());
         }
@@ -168,25 +189,156 @@ impl Drop for Context {
     }
 }
 
-/// render()'s pass loop over the GPU (main.rs:235-290): `frame_limit` passes
-/// of 1 spp each (None = until `keep_going` says stop); after each pass the
-/// accumulated sums and the pass count go to `merge` (Image::merge).
-pub fn render_passes<F, K>(ctx: &mut Context, width: u32, height: u32, max_depth: u32, frame_limit: Option<u32>,
-                           mut merge: F, mut keep_going: K) -> Result<(), MrtError>
+/// The reference's `Image` (main.rs:598-638) kept in HBM: colour sums, depth
+/// sums and the pass count live on the context's device(s) (`mrt_image`);
+/// passes add to it without a host round trip and only `read` / `tonemap`
+/// cross PCIe. On a multi-device context every device keeps its own tiles
+/// and a read gathers them (RCCL over xGMI).
+pub struct GpuImage<'a> {
+    raw: *mut mrt_image,
+    ctx: &'a Context,
+    pub width: u32,
+    pub height: u32,
+}
+
+impl<'a> GpuImage<'a> {
+    pub fn new(ctx: &'a Context, width: u32, height: u32) -> Result<GpuImage<'a>, MrtError> {
+        let mut raw = std::ptr::null_mut();
+        ctx.check(unsafe { mrt_image_create(ctx.raw, width, height, &mut raw) })?;
+        Ok(GpuImage { raw, ctx, width, height })
+    }
+
+    /// Image::clear (main.rs:749-758)
+    pub fn clear(&mut self) -> Result<(), MrtError> {
+        self.ctx.check(unsafe { mrt_image_clear(self.raw) })
+    }
+
+    /// `passes` 1-spp passes merged (Image::merge x passes): samples
+    /// [spp_begin, spp_begin + passes) of every pixel under `seed`.
+    pub fn render(&mut self, seed: u64, spp_begin: u32, passes: u32, max_depth: u32) -> Result<(), MrtError> {
+        self.ctx.check(unsafe { mrt_image_render(self.raw, seed, spp_begin, passes, max_depth, 0) })
+    }
+
+    /// Camera::albedo_normal pre-pass into the image (main.rs:162-222)
+    pub fn prepass(&mut self, seed: u64) -> Result<(), MrtError> {
+        self.ctx.check(unsafe { mrt_image_prepass(self.raw, seed) })
+    }
+
+    /// Sums (w*h*3), depths (w*h); returns the pass count (Image::pixels.0).
+    pub fn read(&mut self, rgb: &mut [f32], bounces: &mut [u32]) -> Result<u32, MrtError> {
+        let n = (self.width * self.height) as usize;
+        assert!(rgb.len() >= 3 * n && bounces.len() >= n);
+        let mut passes = 0u32;
+        self.ctx.check(unsafe { mrt_image_read(self.raw, rgb.as_mut_ptr(), bounces.as_mut_ptr(), &mut passes) })?;
+        Ok(passes)
+    }
+
+    pub fn passes(&mut self) -> Result<u32, MrtError> {
+        let mut passes = 0u32;
+        self.ctx.check(unsafe { mrt_image_read(self.raw, std::ptr::null_mut(), std::ptr::null_mut(), &mut passes) })?;
+        Ok(passes)
+    }
+
+    /// Image::to_rgb_bytes + dump's row flip (main.rs:640-722, 763-766): w*h*3 bytes.
+    pub fn tonemap(&mut self, mode: u32, out: &mut [u8]) -> Result<(), MrtError> {
+        assert!(out.len() >= (self.width * self.height * 3) as usize);
+        self.ctx.check(unsafe { mrt_image_tonemap(self.raw, mode, out.as_mut_ptr()) })
+    }
+}
+
+impl<'a> Drop for GpuImage<'a> {
+    fn drop(&mut self) {
+        unsafe {
+            mrt_image_destroy(self.raw);
+        }
+    }
+}
+
+/// Where a frame's samples come from. The reference's render threads draw
+/// from thread-local fastrand streams seeded afresh for every render() call
+/// (main.rs:167-250), so no two frames share samples. Here sample s of pixel
+/// p is keyed (seed, p, s); the sample index keeps counting across frames,
+/// and the seed moves on when it would wrap.
+#[derive(Debug, Clone, Copy)]
+pub struct SampleStreams {
+    pub seed: u64,
+    pub next_sample: u32,
+}
+
+impl SampleStreams {
+    pub fn new(seed: u64) -> SampleStreams {
+        SampleStreams { seed, next_sample: 0 }
+    }
+
+    /// The (seed, first sample) of the next `n` consecutive samples.
+    pub fn take(&mut self, n: u32) -> (u64, u32) {
+        if self.next_sample as u64 + n as u64 > u32::MAX as u64 {
+            self.seed = self.seed.wrapping_add(1);
+            self.next_sample = 0;
+        }
+        let first = self.next_sample;
+        self.next_sample += n;
+        (self.seed, first)
+    }
+}
+
+/// render()'s worker count: num_cpus - 2, at least 1 (main.rs:159-160).
+pub fn default_workers() -> u32 {
+    let cpus = std::thread::available_parallelism().map(|n| n.get() as i64).unwrap_or(1);
+    (cpus - 2).max(1) as u32
+}
+
+pub struct RenderOptions {
+    pub max_depth: u32,
+    /// the reference's render thread count; `frame_limit` counts passes per worker
+    pub workers: u32,
+    /// 1-spp passes per GPU call (one `update` per batch)
+    pub batch: u32,
+    pub prepass: bool,
+}
+
+impl Default for RenderOptions {
+    fn default() -> RenderOptions {
+        RenderOptions { max_depth: 50, workers: default_workers(), batch: 64, prepass: true }
+    }
+}
+
+/// render(image, event_proxy, world, camera, frame_limit) (main.rs:150-295)
+/// over the GPU, with the reference's accounting:
+///  * the albedo/normal pre-pass first (main.rs:162-222), then Image::clear
+///    (main.rs:233);
+///  * each of `workers` threads renders `frame_limit` whole 1-spp passes
+///    (None: until `keep_going` says stop) and each pass is one merge, so a
+///    frame gets workers * frame_limit passes (main.rs:243-280);
+///  * the passes run `batch` at a time in one mrt_image_render call, and
+///    `update` (the reference's UserEvent::Update, main.rs:274-278) sees the
+///    image after each batch with its pass count;
+///  * `keep_going` is checked before each batch (QUICK_PASS, main.rs:224-231,
+///    282-284).
+/// Returns the passes rendered.
+pub fn render<U, K>(image: &mut GpuImage, streams: &mut SampleStreams, frame_limit: Option<u32>,
+                    opts: &RenderOptions, mut update: U, mut keep_going: K) -> Result<u64, MrtError>
 where
-    F: FnMut(&[f32], &[u32], u32),
+    U: FnMut(&mut GpuImage, u32) -> Result<(), MrtError>,
     K: FnMut() -> bool,
 {
-    let n = (width * height) as usize;
-    let mut rgb = vec![0f32; 3 * n];
-    let mut bounces = vec![0u32; n];
-    let mut pass = 0u32;
-    while frame_limit.map_or(true, |limit| pass < limit) && keep_going() {
-        let args = mrt_render_args { width, height, spp_begin: pass, spp_count: 1, seed: 1, max_depth,
-                                     shard_index: 0, shard_count: 1, flags: 0 };
-        ctx.render(&args, &mut rgb, &mut bounces)?;
-        pass += 1;
-        merge(&rgb, &bounces, pass);
+    if opts.prepass {
+        image.prepass(streams.seed)?;
     }
-    Ok(())
+    image.clear()?;
+    let total = frame_limit.map(|f| f as u64 * opts.workers.max(1) as u64);
+    let batch = opts.batch.max(1) as u64;
+    let mut done = 0u64;
+    while total.map_or(true, |t| done < t) {
+        if !keep_going() {
+            break;
+        }
+        let k = total.map_or(batch, |t| (t - done).min(batch)) as u32;
+        let (seed, first) = streams.take(k);
+        image.render(seed, first, k, opts.max_depth)?;
+        done += k as u64;
+        let passes = image.passes()?;
+        update(image, passes)?;
+    }
+    Ok(done)
 }

@@ -1,4 +1,4 @@
-//! Raw FFI of include/massrt.h, MRT_ABI_VERSION 6.
+//! Raw FFI of include/massrt.h, MRT_ABI_VERSION 7.
 //!
 //! Every struct is `#[repr(C)]` with the header's field order and types;
 //! tests/test_rust_binding.py parses this file and checks each struct's
@@ -8,7 +8,7 @@
 
 use std::os::raw::{c_char, c_void};
 
-pub const MRT_ABI_VERSION: i32 = 6;
+pub const MRT_ABI_VERSION: i32 = 7;
 
 pub const MRT_OK: i32 = 0;
 pub const MRT_ERR_INVALID: i32 = 1;
@@ -261,6 +261,7 @@ pub struct mrt_counters {
     pub wave_slots: u64,
     pub lane_steps: u64,
     pub box_exact: u64,
+    pub shaded: u64,
 }
 
 #[repr(C)]
@@ -283,6 +284,10 @@ pub struct mrt_ctx {
 }
 #[repr(C)]
 pub struct mrt_builder {
+    _private: [u8; 0],
+}
+#[repr(C)]
+pub struct mrt_image {
     _private: [u8; 0],
 }
 
@@ -320,6 +325,24 @@ extern "C" {
     pub fn mrt_shard_unpack_device(ctx: *mut mrt_ctx, width: u32, height: u32, shard_index: u32, shard_count: u32,
                                    d_slab: *const c_void, d_accum_rgb: *mut f32, d_accum_bounces: *mut u32,
                                    hip_stream: *mut c_void) -> i32;
+
+    // ---- one context over several devices (ABI v7)
+    pub fn mrt_create_multi(n_devices: i32, devices: *const i32, out: *mut *mut mrt_ctx) -> i32;
+    pub fn mrt_context_devices(ctx: *mut mrt_ctx, n_devices: *mut i32, devices: *mut i32) -> i32;
+
+    // ---- device-resident Image (main.rs:598-638, ABI v7)
+    pub fn mrt_image_create(ctx: *mut mrt_ctx, width: u32, height: u32, out: *mut *mut mrt_image) -> i32;
+    pub fn mrt_image_destroy(img: *mut mrt_image) -> i32;
+    pub fn mrt_image_clear(img: *mut mrt_image) -> i32;
+    pub fn mrt_image_render(img: *mut mrt_image, seed: u64, spp_begin: u32, passes: u32, max_depth: u32, flags: u32)
+        -> i32;
+    pub fn mrt_image_prepass(img: *mut mrt_image, seed: u64) -> i32;
+    pub fn mrt_image_read(img: *mut mrt_image, rgb: *mut f32, bounces: *mut u32, passes: *mut u32) -> i32;
+    pub fn mrt_image_tonemap(img: *mut mrt_image, mode: u32, rgb8: *mut u8) -> i32;
+    pub fn mrt_image_gather_stats(img: *mut mrt_image, bytes: *mut u64, ms: *mut f64) -> i32;
+
+    // ---- build identity (ABI v7)
+    pub fn mrt_build_info() -> *const c_char;
 
     // ---- host scene builder (C++ mirror of the reference trait surface)
     pub fn mrt_builder_new(rng_seed: u64, out: *mut *mut mrt_builder) -> i32;

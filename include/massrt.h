@@ -20,7 +20,8 @@
  *  - handles are opaque; calls on one context must be serialized by the caller.
  *  - plain C types only (pointers + sizes). Host buffers are caller-owned.
  *    Device memory for the scene is owned by the context.
- *  - one context drives one GPU; multi-GPU = one process (rank) per GPU, each
+ *  - a context drives one GPU (mrt_create) or several (mrt_create_multi, one
+ *    process); multi-process multi-GPU = one process (rank) per GPU, each
  *    rendering its shard of framebuffer tiles (mrt_render_args.shard_*).
  *
  * The reference's Rust side would bind these with `extern "C"` (see
@@ -38,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 6
+#define MRT_ABI_VERSION 7
 
 /* ---- status codes ------------------------------------------------------ */
 #define MRT_OK 0
@@ -253,6 +254,9 @@ typedef struct {
   uint64_t lane_steps;
   /* box tests the early slab decision left to the exact slab test (ABI v6) */
   uint64_t box_exact;
+  /* paths k_shade advanced (one per traced segment shaded by the wavefront
+     loop; the drain hand-off's fused launches shade the rest; ABI v7) */
+  uint64_t shaded;
 } mrt_counters;
 
 /* Kernel timing accumulated by renders flagged MRT_RENDER_TIME_KERNELS
@@ -327,6 +331,59 @@ int mrt_shard_pack_device(mrt_ctx* ctx, uint32_t width, uint32_t height, uint32_
 int mrt_shard_unpack_device(mrt_ctx* ctx, uint32_t width, uint32_t height, uint32_t shard_index,
                             uint32_t shard_count, const void* d_slab, float* d_accum_rgb, uint32_t* d_accum_bounces,
                             void* hip_stream);
+
+/* ---- one context over several devices (ABI v7) --------------
+ * render() (main.rs:150-295) spreads its samples over worker threads that all
+ * merge into ONE Image (main.rs:629-638). The device counterpart: one context
+ * spans n devices (repeats allowed, e.g. {0,0,0} rehearses the exchange on one
+ * GPU). Every device holds the scene; a render splits the frame's 8x8 tiles
+ * over the devices — device i renders shard (shard_index*n + i) of
+ * (shard_count*n), one host thread per device — and the devices' slabs are
+ * gathered onto devices[0] (RCCL send/recv over xGMI when the devices are
+ * distinct, HIP peer copies otherwise; MRT_GATHER=peer|rccl overrides). Every
+ * pixel is summed on one device only, so the image equals the one-device
+ * render bit for bit.
+ * On such a context mrt_upload_scene, mrt_set_camera and mrt_render (host
+ * buffers) use every device; mrt_get/reset_counters and mrt_get/reset_
+ * kernel_stats sum over them; every other entry point runs on devices[0]
+ * (device pointers then live on devices[0]). */
+int mrt_create_multi(int n_devices, const int* devices, mrt_ctx** out);
+/* devices the context spans (1 for mrt_create) and their ordinals (may be NULL) */
+int mrt_context_devices(mrt_ctx* ctx, int* n_devices, int* devices);
+
+/* ---- device-resident Image (main.rs:598-638, ABI v7) --------------------
+ * The reference's Image {pass count, per-pixel (colour sum, depth sum),
+ * albedo, normal} kept in HBM: renders add to it on the device(s) without a
+ * host round trip, and only a read or a tonemap crosses PCIe — the call
+ * pattern of a render() whose passes are batched. On a
+ * multi-device context every device keeps the sums of its own tiles and a
+ * read gathers them. Calls on one image are serialized by the caller. */
+typedef struct mrt_image mrt_image;
+int mrt_image_create(mrt_ctx* ctx, uint32_t width, uint32_t height, mrt_image** out);
+int mrt_image_destroy(mrt_image* img);
+/* Image::clear (main.rs:749-758): sums, depths and the pass count to 0 */
+int mrt_image_clear(mrt_image* img);
+/* `passes` 1-spp passes merged (Image::merge x passes, main.rs:253-273):
+ * sample s in [spp_begin, spp_begin + passes) of every pixel, keyed (seed,
+ * pixel, s) as in mrt_render; the pass count grows by `passes`. flags:
+ * MRT_RENDER_COUNTERS / MRT_RENDER_TIME_KERNELS. Enqueued: returns once the
+ * work is queued on every device (a read or tonemap waits for it). */
+int mrt_image_render(mrt_image* img, uint64_t seed, uint32_t spp_begin, uint32_t passes, uint32_t max_depth,
+                     uint32_t flags);
+/* Camera::albedo_normal pre-pass into the image (main.rs:162-222; as mrt_prepass) */
+int mrt_image_prepass(mrt_image* img, uint64_t seed);
+/* sums (W*H*3 f32) and depths (W*H u32) — either may be NULL — and the pass count */
+int mrt_image_read(mrt_image* img, float* rgb, uint32_t* bounces, uint32_t* passes);
+/* Image::to_rgb_bytes + dump's row flip (as mrt_tonemap) on devices[0]: W*H*3
+ * bytes, top row first. ALBEDO / NORMAL show the pre-pass (zeros before one). */
+int mrt_image_tonemap(mrt_image* img, uint32_t mode, uint8_t* rgb8);
+/* bytes that crossed between devices in the image's gathers, and their time */
+int mrt_image_gather_stats(mrt_image* img, uint64_t* bytes, double* ms);
+
+/* ---- build identity (ABI v7) -------------------------------------------
+ * hash of the sources the library was built from (csrc/ + include/, as
+ * tools/src_hash.py computes it), so a run can prove it loaded HEAD's code */
+const char* mrt_build_info(void);
 
 /* ---- host scene builder (C++ mirror of the reference trait surface) -----
  * A builder owns a World under construction plus the scene RNG (fastrand

@@ -1,0 +1,519 @@
+// frames.hip — one context over several devices, and the device-resident
+// Image (include/massrt.h, ABI v7).
+//
+// The reference's render() (main.rs:150-295) runs num_cpus-2 worker threads
+// that each render whole 1-spp passes and merge them into ONE Image
+// (main.rs:629-638). Here the workers are devices: a frame's 8x8 tiles are
+// split over the devices of a context (device i renders shard si + i*sc of
+// sc*n, one host thread per device, each through the single-device path of
+// render.hip), every device keeps the sums of its own tiles in its own HBM,
+// and a read gathers the devices' tile slabs onto the first device — RCCL
+// send/recv over xGMI between distinct devices, HIP peer copies otherwise —
+// where they are unpacked. Every pixel is summed on one device only, in
+// sample order, so the image equals the one-device render bit for bit.
+//
+// This file uses only the public single-device entry points on the
+// per-device contexts (mrt_render_device, mrt_shard_pack/unpack_device,
+// mrt_prepass_device, mrt_tonemap_device); render.hip routes the entry
+// points of a multi-device handle here (frames.h).
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "frames.h"
+
+int massrt_ctx_device(const mrt_ctx* ctx);  // render.hip
+
+namespace {
+
+struct Fail {
+  int code;
+  std::string msg;
+};
+
+#define HIPF(x)                                                                                 \
+  do {                                                                                          \
+    hipError_t e_ = (x);                                                                        \
+    if (e_ != hipSuccess) throw Fail{MRT_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+#define MRTF(ctx, x)                                \
+  do {                                              \
+    int r_ = (x);                                   \
+    if (r_ != MRT_OK) throw Fail{r_, mrt_last_error(ctx)}; \
+  } while (0)
+// RCCL is opened on first use (dlopen), not linked: a process that never
+// gathers over RCCL (one device, peer copies, every test on a 1-GPU box)
+// does not load it next to the HIP runtime its host (e.g. torch) brings.
+struct Rccl {
+  ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+const Rccl& rccl() {
+  static Rccl r;
+  static bool tried = false;
+  if (!tried) {
+    tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (h) {
+      r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
+      r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+      r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+      r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+      r.send = (decltype(r.send))dlsym(h, "ncclSend");
+      r.recv = (decltype(r.recv))dlsym(h, "ncclRecv");
+      r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+    }
+  }
+  if (!r.comm_init_all || !r.group_start || !r.group_end || !r.send || !r.recv || !r.error_string)
+    throw Fail{MRT_ERR_HIP, "RCCL (librccl.so.1) is not available; MRT_GATHER=peer uses HIP peer copies"};
+  return r;
+}
+
+#define NCCLF(x)                                                                                     \
+  do {                                                                                               \
+    ncclResult_t r_ = (x);                                                                           \
+    if (r_ != ncclSuccess) throw Fail{MRT_ERR_HIP, std::string(#x) + ": " + rccl().error_string(r_)}; \
+  } while (0)
+
+bool valid_size(uint32_t W, uint32_t H) { return W && H && (uint64_t)W * H < (1ull << 32); }
+
+// One device's part of a frame: the accumulation buffers (full frame size;
+// only this device's tiles are written), its tile slab and, on device 0, the
+// buffer its slab is received into.
+struct DevFrame {
+  mrt_ctx* ctx = nullptr;
+  int device = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t ev = nullptr;
+  float* rgb = nullptr;
+  uint32_t* b = nullptr;
+  void* slab = nullptr;
+  uint32_t count = 0;  // pixels of this device's shard
+  void* recv = nullptr;  // on device 0
+};
+
+// A frame over the devices of a context: device i owns shard si + i*sc of sc*n.
+struct Frame {
+  std::vector<DevFrame> d;
+  MultiDev* m = nullptr;  // transport (null: one device)
+  uint32_t W = 0, H = 0, si = 0, sc = 1;
+  uint64_t gather_bytes = 0;
+  double gather_ms = 0;
+
+  uint32_t shard(size_t i) const { return si + (uint32_t)i * sc; }
+  uint32_t shards() const { return sc * (uint32_t)d.size(); }
+  size_t npix() const { return (size_t)W * H; }
+
+  void setup(MultiDev* mm, const std::vector<mrt_ctx*>& ctxs, uint32_t w, uint32_t h, uint32_t s_i, uint32_t s_c) {
+    release();
+    m = ctxs.size() > 1 ? mm : nullptr;
+    W = w, H = h, si = s_i, sc = s_c ? s_c : 1;
+    d.resize(ctxs.size());
+    for (size_t i = 0; i < d.size(); ++i) {
+      DevFrame& f = d[i];
+      f.ctx = ctxs[i];
+      f.device = massrt_ctx_device(f.ctx);
+      HIPF(hipSetDevice(f.device));
+      HIPF(hipStreamCreateWithFlags(&f.st, hipStreamNonBlocking));
+      HIPF(hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
+      HIPF(hipMalloc(&f.rgb, npix() * 12));
+      HIPF(hipMalloc(&f.b, npix() * 4));
+      if (d.size() > 1) {
+        MRTF(f.ctx, mrt_shard_pixels(W, H, shard(i), shards(), nullptr, &f.count));
+        HIPF(hipMalloc(&f.slab, (size_t)f.count * 16 + 16));
+      }
+    }
+    HIPF(hipSetDevice(d[0].device));
+    for (size_t i = 1; i < d.size(); ++i) HIPF(hipMalloc(&d[i].recv, (size_t)d[i].count * 16 + 16));
+    clear();
+  }
+
+  void clear() {
+    for (DevFrame& f : d) {
+      HIPF(hipSetDevice(f.device));
+      HIPF(hipMemsetAsync(f.rgb, 0, npix() * 12, f.st));
+      HIPF(hipMemsetAsync(f.b, 0, npix() * 4, f.st));
+    }
+  }
+
+  void release() {
+    for (DevFrame& f : d) {
+      hipSetDevice(f.device);
+      if (f.st) hipStreamSynchronize(f.st);
+    }
+    for (DevFrame& f : d) {
+      hipSetDevice(f.device);
+      hipFree(f.rgb), hipFree(f.b), hipFree(f.slab);
+      if (f.ev) hipEventDestroy(f.ev);
+      if (f.st) hipStreamDestroy(f.st);
+    }
+    if (!d.empty()) {
+      hipSetDevice(d[0].device);
+      for (DevFrame& f : d) hipFree(f.recv);
+    }
+    d.clear();
+  }
+
+  ~Frame() { release(); }
+
+  // every device renders its shard of `a` (a.shard_* ignored), concurrently
+  void render(const mrt_render_args& a0) {
+    if (d.size() == 1) {
+      mrt_render_args a = a0;
+      a.shard_index = si, a.shard_count = sc;
+      MRTF(d[0].ctx, mrt_render_device(d[0].ctx, &a, d[0].rgb, d[0].b, d[0].st));
+      return;
+    }
+    std::vector<Fail> fails(d.size(), Fail{MRT_OK, ""});
+    std::vector<std::thread> th;
+    for (size_t i = 0; i < d.size(); ++i)
+      th.emplace_back([&, i] {
+        mrt_render_args a = a0;
+        a.shard_index = shard(i), a.shard_count = shards();
+        const int rc = mrt_render_device(d[i].ctx, &a, d[i].rgb, d[i].b, d[i].st);
+        if (rc != MRT_OK) fails[i] = Fail{rc, mrt_last_error(d[i].ctx)};
+      });
+    for (auto& t : th) t.join();
+    for (const Fail& f : fails)
+      if (f.code != MRT_OK) throw f;
+  }
+
+  // the other devices' tiles onto device 0's buffers (pack, send, unpack)
+  void gather();
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+struct MultiDev {
+  std::vector<mrt_ctx*> devs;
+  std::vector<int> ids;
+  bool rccl = false;
+  std::vector<ncclComm_t> comms;  // lazily, at the first RCCL gather
+  Frame* scratch = nullptr;       // mrt_render's frame (host buffers)
+};
+
+namespace {
+
+void ensure_comms(MultiDev* m) {
+  if (!m->comms.empty()) return;
+  m->comms.resize(m->ids.size());
+  const Rccl& R = rccl();
+  const ncclResult_t r = R.comm_init_all(m->comms.data(), (int)m->ids.size(), m->ids.data());
+  if (r != ncclSuccess) {
+    m->comms.clear();
+    throw Fail{MRT_ERR_HIP, std::string("ncclCommInitAll: ") + R.error_string(r)};
+  }
+}
+
+void Frame::gather() {
+  if (d.size() < 2) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (size_t i = 1; i < d.size(); ++i)
+    if (d[i].count) MRTF(d[i].ctx, mrt_shard_pack_device(d[i].ctx, W, H, shard(i), shards(), d[i].rgb, d[i].b, d[i].slab, d[i].st));
+  uint64_t bytes = 0;
+  if (m && m->rccl) {
+    ensure_comms(m);
+    const Rccl& R = rccl();
+    NCCLF(R.group_start());
+    for (size_t i = 1; i < d.size(); ++i) {
+      if (!d[i].count) continue;
+      NCCLF(R.send(d[i].slab, (size_t)d[i].count * 4, ncclUint32, 0, m->comms[i], d[i].st));
+      NCCLF(R.recv(d[i].recv, (size_t)d[i].count * 4, ncclUint32, (int)i, m->comms[0], d[0].st));
+      bytes += (uint64_t)d[i].count * 16;
+    }
+    NCCLF(R.group_end());
+  } else {
+    for (size_t i = 1; i < d.size(); ++i) {
+      if (!d[i].count) continue;
+      HIPF(hipSetDevice(d[i].device));
+      HIPF(hipEventRecord(d[i].ev, d[i].st));
+      HIPF(hipSetDevice(d[0].device));
+      HIPF(hipStreamWaitEvent(d[0].st, d[i].ev, 0));
+      HIPF(hipMemcpyPeerAsync(d[i].recv, d[0].device, d[i].slab, d[i].device, (size_t)d[i].count * 16, d[0].st));
+      bytes += (uint64_t)d[i].count * 16;
+    }
+  }
+  for (size_t i = 1; i < d.size(); ++i)
+    if (d[i].count)
+      MRTF(d[0].ctx, mrt_shard_unpack_device(d[0].ctx, W, H, shard(i), shards(), d[i].recv, d[0].rgb, d[0].b, d[0].st));
+  HIPF(hipSetDevice(d[0].device));
+  HIPF(hipStreamSynchronize(d[0].st));
+  gather_bytes += bytes;
+  gather_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+std::vector<mrt_ctx*> devices_of(mrt_ctx* ctx) {
+  MultiDev* m = ctx_multi(ctx);
+  return m ? m->devs : std::vector<mrt_ctx*>{ctx};
+}
+
+template <typename F>
+int guard(mrt_ctx* ctx, F&& f) {
+  try {
+    f();
+    return MRT_OK;
+  } catch (const Fail& e) {
+    ctx_set_error(ctx, e.msg);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    ctx_set_error(ctx, "out of host memory");
+    return MRT_ERR_NOMEM;
+  } catch (const std::exception& e) {
+    ctx_set_error(ctx, e.what());
+    return MRT_ERR_INVALID;
+  }
+}
+
+}  // namespace
+
+// ---- render.hip's side of a multi-device handle (frames.h) -----------------
+int multi_count(const MultiDev* m) { return (int)m->devs.size(); }
+mrt_ctx* multi_dev(const MultiDev* m, int i) { return m->devs[(size_t)i]; }
+
+void multi_free(MultiDev* m) {
+  if (!m) return;
+  delete m->scratch;
+  if (!m->comms.empty() && rccl().comm_destroy)
+    for (ncclComm_t c : m->comms) rccl().comm_destroy(c);
+  for (mrt_ctx* c : m->devs) mrt_destroy(c);
+  delete m;
+}
+
+int multi_render(MultiDev* m, const mrt_render_args* a, float* rgb, uint32_t* bounces, std::string& err) {
+  try {
+    if (!a || !rgb || !bounces) throw Fail{MRT_ERR_INVALID, "null argument"};
+    if (!valid_size(a->width, a->height)) throw Fail{MRT_ERR_INVALID, "bad image size"};
+    const uint32_t sc = a->shard_count ? a->shard_count : 1;
+    if (a->shard_index >= sc) throw Fail{MRT_ERR_INVALID, "shard_index >= shard_count"};
+    if (!m->scratch) m->scratch = new Frame();
+    Frame& f = *m->scratch;
+    if (f.d.empty() || f.W != a->width || f.H != a->height || f.si != a->shard_index || f.sc != sc)
+      f.setup(m, m->devs, a->width, a->height, a->shard_index, sc);
+    const size_t n = f.npix();
+    // every device starts from the caller's sums (its shard's pixels of them
+    // are what it adds to); device 0's buffer comes back whole
+    for (DevFrame& d : f.d) {
+      HIPF(hipSetDevice(d.device));
+      HIPF(hipMemcpyAsync(d.rgb, rgb, n * 12, hipMemcpyHostToDevice, d.st));
+      HIPF(hipMemcpyAsync(d.b, bounces, n * 4, hipMemcpyHostToDevice, d.st));
+    }
+    f.render(*a);
+    f.gather();
+    HIPF(hipSetDevice(f.d[0].device));
+    HIPF(hipMemcpyAsync(rgb, f.d[0].rgb, n * 12, hipMemcpyDeviceToHost, f.d[0].st));
+    HIPF(hipMemcpyAsync(bounces, f.d[0].b, n * 4, hipMemcpyDeviceToHost, f.d[0].st));
+    HIPF(hipStreamSynchronize(f.d[0].st));
+    return MRT_OK;
+  } catch (const Fail& e) {
+    err = e.msg;
+    return e.code;
+  } catch (const std::exception& e) {
+    err = e.what();
+    return MRT_ERR_INVALID;
+  }
+}
+
+// ---- the device-resident Image ----------------------------------------------
+struct mrt_image {
+  mrt_ctx* ctx = nullptr;
+  Frame f;
+  uint32_t passes = 0;
+  bool gathered = true;  // device 0's buffers hold every device's tiles
+  float* aux = nullptr;  // device 0: albedo then normal (W*H*3 each), zero before a pre-pass
+  uint8_t* rgb8 = nullptr;  // device 0: display bytes
+};
+
+extern "C" {
+
+int mrt_create_multi(int n, const int* devices, mrt_ctx** out) {
+  if (!out || !devices || n < 1) {
+    ctx_set_error(nullptr, "mrt_create_multi: need n >= 1 devices and an output pointer");
+    return MRT_ERR_INVALID;
+  }
+  *out = nullptr;
+  MultiDev* m = new MultiDev();
+  m->ids.assign(devices, devices + n);
+  for (int i = 0; i < n; ++i) {
+    mrt_ctx* c = nullptr;
+    const int rc = mrt_create(devices[i], &c);
+    if (rc != MRT_OK) {  // mrt_create left its message in the global error
+      const std::string msg = mrt_global_last_error();
+      multi_free(m);
+      ctx_set_error(nullptr, msg);
+      return rc;
+    }
+    m->devs.push_back(c);
+  }
+  std::vector<int> sorted = m->ids;
+  std::sort(sorted.begin(), sorted.end());
+  const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+  const char* g = getenv("MRT_GATHER");
+  const std::string mode = g ? g : "";
+  if (mode == "rccl" && !distinct) {
+    multi_free(m);
+    ctx_set_error(nullptr, "MRT_GATHER=rccl needs distinct devices (RCCL has one rank per device)");
+    return MRT_ERR_INVALID;
+  }
+  m->rccl = n > 1 && distinct && mode != "peer";
+  // xGMI peer access from device 0 to the others and back (peer copies and
+  // RCCL's P2P transport); already-enabled is fine
+  for (int i = 1; i < n; ++i) {
+    if (devices[i] == devices[0]) continue;
+    hipSetDevice(devices[0]);
+    hipDeviceEnablePeerAccess(devices[i], 0);
+    hipSetDevice(devices[i]);
+    hipDeviceEnablePeerAccess(devices[0], 0);
+  }
+  (void)hipGetLastError();
+  *out = ctx_wrap_multi(m);
+  return MRT_OK;
+}
+
+int mrt_context_devices(mrt_ctx* ctx, int* n, int* devices) {
+  if (!ctx || !n) {
+    ctx_set_error(ctx, "null argument");
+    return MRT_ERR_INVALID;
+  }
+  if (MultiDev* m = ctx_multi(ctx)) {
+    *n = (int)m->ids.size();
+    if (devices) std::copy(m->ids.begin(), m->ids.end(), devices);
+  } else {
+    *n = 1;
+    if (devices) devices[0] = massrt_ctx_device(ctx);
+  }
+  return MRT_OK;
+}
+
+int mrt_image_create(mrt_ctx* ctx, uint32_t W, uint32_t H, mrt_image** out) {
+  if (!ctx || !out) {
+    ctx_set_error(ctx, "null argument");
+    return MRT_ERR_INVALID;
+  }
+  *out = nullptr;
+  auto img = std::make_unique<mrt_image>();
+  img->ctx = ctx;
+  const int rc = guard(ctx, [&] {
+    if (!valid_size(W, H)) throw Fail{MRT_ERR_INVALID, "bad image size"};
+    img->f.setup(ctx_multi(ctx), devices_of(ctx), W, H, 0, 1);
+    HIPF(hipSetDevice(img->f.d[0].device));
+    HIPF(hipStreamSynchronize(img->f.d[0].st));
+  });
+  if (rc == MRT_OK) *out = img.release();
+  return rc;
+}
+
+int mrt_image_destroy(mrt_image* img) {
+  if (!img) return MRT_OK;
+  if (!img->f.d.empty()) {
+    hipSetDevice(img->f.d[0].device);
+    if (img->f.d[0].st) hipStreamSynchronize(img->f.d[0].st);
+    hipFree(img->aux);
+    hipFree(img->rgb8);
+  }
+  delete img;
+  return MRT_OK;
+}
+
+int mrt_image_clear(mrt_image* img) {
+  if (!img) return MRT_ERR_INVALID;
+  return guard(img->ctx, [&] {
+    img->f.clear();
+    img->passes = 0;
+    img->gathered = true;
+  });
+}
+
+int mrt_image_render(mrt_image* img, uint64_t seed, uint32_t spp_begin, uint32_t passes, uint32_t max_depth,
+                     uint32_t flags) {
+  if (!img) return MRT_ERR_INVALID;
+  return guard(img->ctx, [&] {
+    if ((uint64_t)spp_begin + passes > 0xFFFFFFFFull) throw Fail{MRT_ERR_INVALID, "sample index overflow"};
+    if ((uint64_t)img->passes + passes > 0xFFFFFFFFull) throw Fail{MRT_ERR_INVALID, "pass count overflow"};
+    if (flags & ~(uint32_t)(MRT_RENDER_COUNTERS | MRT_RENDER_TIME_KERNELS))
+      throw Fail{MRT_ERR_INVALID, "mrt_image_render takes MRT_RENDER_COUNTERS / MRT_RENDER_TIME_KERNELS only"};
+    if (!passes) return;
+    mrt_render_args a{img->f.W, img->f.H, spp_begin, passes, seed, max_depth, 0, 1, flags};
+    img->f.render(a);
+    img->passes += passes;
+    img->gathered = img->f.d.size() == 1;
+  });
+}
+
+int mrt_image_prepass(mrt_image* img, uint64_t seed) {
+  if (!img) return MRT_ERR_INVALID;
+  return guard(img->ctx, [&] {
+    DevFrame& d0 = img->f.d[0];
+    const size_t n = img->f.npix();
+    HIPF(hipSetDevice(d0.device));
+    if (!img->aux) HIPF(hipMalloc(&img->aux, n * 24));
+    MRTF(d0.ctx, mrt_prepass_device(d0.ctx, img->f.W, img->f.H, seed, img->aux, img->aux + 3 * n, d0.st));
+  });
+}
+
+int mrt_image_read(mrt_image* img, float* rgb, uint32_t* bounces, uint32_t* passes) {
+  if (!img) return MRT_ERR_INVALID;
+  return guard(img->ctx, [&] {
+    if (!img->gathered) {
+      img->f.gather();
+      img->gathered = true;
+    }
+    DevFrame& d0 = img->f.d[0];
+    const size_t n = img->f.npix();
+    HIPF(hipSetDevice(d0.device));
+    if (rgb) HIPF(hipMemcpyAsync(rgb, d0.rgb, n * 12, hipMemcpyDeviceToHost, d0.st));
+    if (bounces) HIPF(hipMemcpyAsync(bounces, d0.b, n * 4, hipMemcpyDeviceToHost, d0.st));
+    HIPF(hipStreamSynchronize(d0.st));
+    if (passes) *passes = img->passes;
+  });
+}
+
+int mrt_image_tonemap(mrt_image* img, uint32_t mode, uint8_t* out) {
+  if (!img) return MRT_ERR_INVALID;
+  return guard(img->ctx, [&] {
+    if (!out) throw Fail{MRT_ERR_INVALID, "null output"};
+    if (mode > MRT_DISPLAY_NORMAL) throw Fail{MRT_ERR_INVALID, "bad display mode"};
+    const bool aux = mode == MRT_DISPLAY_ALBEDO || mode == MRT_DISPLAY_NORMAL;
+    DevFrame& d0 = img->f.d[0];
+    const size_t n = img->f.npix();
+    if (!aux && !img->gathered) {
+      img->f.gather();
+      img->gathered = true;
+    }
+    HIPF(hipSetDevice(d0.device));
+    if (!img->rgb8) HIPF(hipMalloc(&img->rgb8, n * 3));
+    if (aux && !img->aux) {  // Image::to_rgb_bytes: no buffer yet -> zeros
+      HIPF(hipMemsetAsync(img->rgb8, 0, n * 3, d0.st));
+    } else {
+      const float* src = aux ? img->aux + (mode == MRT_DISPLAY_NORMAL ? 3 * n : 0) : d0.rgb;
+      MRTF(d0.ctx, mrt_tonemap_device(d0.ctx, img->f.W, img->f.H, src, d0.b, img->passes, mode, img->rgb8, d0.st));
+    }
+    HIPF(hipMemcpyAsync(out, img->rgb8, n * 3, hipMemcpyDeviceToHost, d0.st));
+    HIPF(hipStreamSynchronize(d0.st));
+  });
+}
+
+int mrt_image_gather_stats(mrt_image* img, uint64_t* bytes, double* ms) {
+  if (!img) return MRT_ERR_INVALID;
+  if (bytes) *bytes = img->f.gather_bytes;
+  if (ms) *ms = img->f.gather_ms;
+  return MRT_OK;
+}
+
+}  // extern "C"

@@ -27,7 +27,7 @@ MRT_DEV uint32_t make_ref(uint32_t kind, uint32_t idx) { return (kind << 28) | i
 
 struct DevCounters {
   unsigned long long samples, segments, node_visits, sphere_tests, triangle_tests, instance_entries,
-      model_entries, closest_hits, texel_taps, bounces, wave_slots, lane_steps, box_exact;
+      model_entries, closest_hits, texel_taps, bounces, wave_slots, lane_steps, box_exact, shaded;
 };
 
 struct LocalCounters {

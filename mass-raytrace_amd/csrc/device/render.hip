@@ -24,6 +24,7 @@
 
 #include "../../../include/massrt.h"
 #include "../host/display.h"
+#include "frames.h"
 #include "path.h"
 #include "upload.h"
 
@@ -114,12 +115,12 @@ __device__ __forceinline__ uint32_t wg_reserve(uint32_t* counter, uint32_t count
 }
 
 __device__ void flush_counters(DevCounters* c, const LocalCounters& lc, uint32_t segs, uint32_t hits,
-                               uint32_t samples, uint32_t bounces) {
-  uint32_t v[13] = {samples, segs, lc.node_visits, lc.sphere_tests, lc.triangle_tests, lc.instance_entries,
-                    lc.model_entries, hits, lc.texel_taps, bounces, lc.wave_slots, lc.lane_steps, lc.box_exact};
+                               uint32_t samples, uint32_t bounces, uint32_t shaded = 0) {
+  uint32_t v[14] = {samples, segs, lc.node_visits, lc.sphere_tests, lc.triangle_tests, lc.instance_entries,
+                    lc.model_entries, hits, lc.texel_taps, bounces, lc.wave_slots, lc.lane_steps, lc.box_exact, shaded};
   unsigned long long* dst = reinterpret_cast<unsigned long long*>(c);
 #pragma unroll
-  for (int k = 0; k < 13; ++k) {
+  for (int k = 0; k < 14; ++k) {
     uint32_t s = wave_sum(v[k]);
     if (lane_id() == 0 && s) atomicAdd(dst + k, (unsigned long long)s);
   }
@@ -398,68 +399,72 @@ __global__ __launch_bounds__(kBlock, MRT_SHADE_WPE) void k_shade(DevScene S, Dev
                                                   uint32_t* work, float4* results, DevCounters* cnt) {
   const uint32_t n = ctrl->active[cur];
   if (blockIdx.x == 0 && threadIdx.x < kGroups) ctrl->group_next[threadIdx.x * 32] = 0;  // next k_trace
-  const uint32_t base = blockIdx.x * kBlock;
-  if (base >= n) return;
-  const uint32_t i = base + threadIdx.x;
   LocalCounters lc;
-  bool alive = false, need = false;
-  float4 ro{}, rd{}, thr{}, rad{};
-  uint4 rs{};
-  uint32_t nbounce = 0, nsample = 0;
-  if (i < n) {
-    ro = in.ro[i];
-    rd = in.rd[i];
-    thr = in.thr[i];
-    rad = in.rad[i];
-    rs = in.rng[i];
-    const uint4 hv = hits[i];
-    Hit h{__uint_as_float(hv.x), hv.y, hv.z};
-    V3 o{ro.x, ro.y, ro.z}, d{rd.x, rd.y, rd.z}, T{thr.x, thr.y, thr.z}, L{rad.x, rad.y, rad.z};
-    uint32_t g = __float_as_uint(ro.w), k = __float_as_uint(rd.w);
-    PathRng rng{(unsigned long long)rs.x | ((unsigned long long)rs.y << 32),
-                (unsigned long long)rs.z | ((unsigned long long)rs.w << 32)};
-    const bool cont = shade_step<EXT>(S, rp.max_depth, h, o, d, T, L, k, rng, lc, nbounce);
-    if (cont) {
-      alive = true;
-      ro = make_float4(o.x, o.y, o.z, __uint_as_float(g));
-      rd = make_float4(d.x, d.y, d.z, __uint_as_float(k));
-      thr = make_float4(T.x, T.y, T.z, 0.0f);
-      rad = make_float4(L.x, L.y, L.z, 0.0f);
-      rs = make_uint4((uint32_t)rng.s0, (uint32_t)(rng.s0 >> 32), (uint32_t)rng.s1, (uint32_t)(rng.s1 >> 32));
-    } else {
-      results[MRT_IDX(S, g, rp.G, 21)] = make_float4(L.x, L.y, L.z, __uint_as_float(k));
-      need = true;
-      nsample = 1;
-    }
-  }
-  // regenerate finished slots from the work counter and compact survivors
-  // into the next pool: one atomic per workgroup for each (same-address
-  // atomics from every wave serialise in L2)
+  uint32_t nbounce = 0, nsample = 0, nshaded = 0;
   __shared__ uint32_t s_cnt[kWaves], s_base;
   const uint32_t wave = threadIdx.x / 64;
-  const unsigned long long need_mask = __ballot(need);
-  const uint32_t wbase = wg_reserve(work, (uint32_t)__popcll(need_mask), wave, s_cnt, s_base);
-  if (need) {
-    uint32_t g = wbase + lane_rank(need_mask);
-    if (g < rp.G) {
-      gen_work(cam, rp, g, ro, rd, rs);
-      thr = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-      rad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      alive = true;
+  // grid-stride over the live pool: the grid is sized to the GPU, not to the
+  // pool's capacity, so a drain launch with few live paths does not dispatch
+  // (and retire) a workgroup per 256 slots of a 64M-slot pool
+  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {  // uniform per workgroup
+    const uint32_t i = base + threadIdx.x;
+    bool alive = false, need = false;
+    float4 ro{}, rd{}, thr{}, rad{};
+    uint4 rs{};
+    if (i < n) {
+      nshaded += 1;
+      ro = in.ro[i];
+      rd = in.rd[i];
+      thr = in.thr[i];
+      rad = in.rad[i];
+      rs = in.rng[i];
+      const uint4 hv = hits[i];
+      Hit h{__uint_as_float(hv.x), hv.y, hv.z};
+      V3 o{ro.x, ro.y, ro.z}, d{rd.x, rd.y, rd.z}, T{thr.x, thr.y, thr.z}, L{rad.x, rad.y, rad.z};
+      uint32_t g = __float_as_uint(ro.w), k = __float_as_uint(rd.w);
+      PathRng rng{(unsigned long long)rs.x | ((unsigned long long)rs.y << 32),
+                  (unsigned long long)rs.z | ((unsigned long long)rs.w << 32)};
+      const bool cont = shade_step<EXT>(S, rp.max_depth, h, o, d, T, L, k, rng, lc, nbounce);
+      if (cont) {
+        alive = true;
+        ro = make_float4(o.x, o.y, o.z, __uint_as_float(g));
+        rd = make_float4(d.x, d.y, d.z, __uint_as_float(k));
+        thr = make_float4(T.x, T.y, T.z, 0.0f);
+        rad = make_float4(L.x, L.y, L.z, 0.0f);
+        rs = make_uint4((uint32_t)rng.s0, (uint32_t)(rng.s0 >> 32), (uint32_t)rng.s1, (uint32_t)(rng.s1 >> 32));
+      } else {
+        results[MRT_IDX(S, g, rp.G, 21)] = make_float4(L.x, L.y, L.z, __uint_as_float(k));
+        need = true;
+        nsample += 1;
+      }
+    }
+    // regenerate finished slots from the work counter and compact survivors
+    // into the next pool: one atomic per workgroup for each (same-address
+    // atomics from every wave serialise in L2)
+    const unsigned long long need_mask = __ballot(need);
+    const uint32_t wbase = wg_reserve(work, (uint32_t)__popcll(need_mask), wave, s_cnt, s_base);
+    if (need) {
+      uint32_t g = wbase + lane_rank(need_mask);
+      if (g < rp.G) {
+        gen_work(cam, rp, g, ro, rd, rs);
+        thr = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+        rad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        alive = true;
+      }
+    }
+    // compact survivors + new paths into the next pool
+    const unsigned long long alive_mask = __ballot(alive);
+    const uint32_t obase = wg_reserve(&ctrl->active[cur ^ 1], (uint32_t)__popcll(alive_mask), wave, s_cnt, s_base);
+    if (alive) {
+      uint32_t pos = MRT_IDX(S, obase + lane_rank(alive_mask), rp.pool_cap, 22);
+      out.ro[pos] = ro;
+      out.rd[pos] = rd;
+      out.thr[pos] = thr;
+      out.rad[pos] = rad;
+      out.rng[pos] = rs;
     }
   }
-  // compact survivors + new paths into the next pool
-  const unsigned long long alive_mask = __ballot(alive);
-  const uint32_t obase = wg_reserve(&ctrl->active[cur ^ 1], (uint32_t)__popcll(alive_mask), wave, s_cnt, s_base);
-  if (alive) {
-    uint32_t pos = MRT_IDX(S, obase + lane_rank(alive_mask), rp.pool_cap, 22);
-    out.ro[pos] = ro;
-    out.rd[pos] = rd;
-    out.thr[pos] = thr;
-    out.rad[pos] = rad;
-    out.rng[pos] = rs;
-  }
-  if (COUNT) flush_counters(cnt, lc, 0, 0, nsample, nbounce);
+  if (COUNT) flush_counters(cnt, lc, 0, 0, nsample, nbounce, nshaded);
 }
 
 // The whole path loop in one persistent kernel: every lane owns a path
@@ -894,6 +899,7 @@ struct Queue {
 
 struct mrt_ctx {
   int device = 0;
+  MultiDev* multi = nullptr;  // a context over several devices (frames.hip): the rest is unused
   hipStream_t stream = nullptr;
   std::string err;
   // scene
@@ -980,6 +986,51 @@ struct mrt_ctx {
 };
 
 static thread_local std::string g_last_error;
+
+static int massrt_ctx_device_of(const mrt_ctx* c) { return c->device; }
+
+mrt_ctx* ctx_wrap_multi(MultiDev* m) {
+  mrt_ctx* c = new mrt_ctx();
+  c->multi = m;
+  c->device = massrt_ctx_device_of(multi_dev(m, 0));
+  return c;
+}
+MultiDev* ctx_multi(const mrt_ctx* c) { return c ? c->multi : nullptr; }
+void ctx_set_error(mrt_ctx* c, const std::string& msg) {
+  if (c)
+    c->err = msg;
+  else
+    g_last_error = msg;
+}
+
+namespace {
+// A multi-device handle (mrt_create_multi): entry points that act on one
+// device run on device 0; scene and camera go to every device.
+template <typename F>
+int on_dev0(mrt_ctx* c, F&& f) {
+  mrt_ctx* d = multi_dev(c->multi, 0);
+  const int rc = f(d);
+  c->err = d->err;
+  return rc;
+}
+template <typename F>
+int on_each(mrt_ctx* c, F&& f) {
+  for (int i = 0; i < multi_count(c->multi); ++i) {
+    mrt_ctx* d = multi_dev(c->multi, i);
+    const int rc = f(d);
+    if (rc != MRT_OK) {
+      c->err = d->err;
+      return rc;
+    }
+  }
+  c->err.clear();
+  return MRT_OK;
+}
+}  // namespace
+#define MRT_DEV0(c, call) \
+  if ((c) && (c)->multi) return on_dev0((c), [&](mrt_ctx* c) { return call; })
+#define MRT_EACH(c, call) \
+  if ((c) && (c)->multi) return on_each((c), [&](mrt_ctx* c) { return call; })
 
 namespace {
 
@@ -1101,6 +1152,28 @@ void launch_trace(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in
       launch_trace_v<false, 0>(c, st, q, in, cur, count, tmin, tmax);
   }
   HIP_CHECK(hipGetLastError());
+}
+
+// k_shade's grid: it strides over the live pool, so enough workgroups to
+// fill every CU at its occupancy (MRT_SHADE_WGS_PER_CU overrides), never
+// more than the pool's capacity needs.
+uint32_t shade_grid(mrt_ctx* c, bool count) {
+  const void* f = count ? (c->scene_ext ? (const void*)k_shade<true, true> : (const void*)k_shade<true, false>)
+                        : (c->scene_ext ? (const void*)k_shade<false, true> : (const void*)k_shade<false, false>);
+  auto key = std::make_pair(f, (size_t)1);  // (kernel, tag) in the persistent-grid cache
+  auto it = c->grids.find(key);
+  uint32_t g = 0;
+  if (it != c->grids.end()) {
+    g = it->second;
+  } else {
+    int per_cu = 0;
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, 0));
+    if (const char* e = getenv("MRT_SHADE_WGS_PER_CU")) per_cu = atoi(e);
+    g = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
+    c->grids[key] = g;
+  }
+  const uint32_t need = (uint32_t)((c->q[0].cap + kBlock - 1) / kBlock);
+  return std::max<uint32_t>(1, std::min(g, need));
 }
 
 // P paths per queue set (n_queues queues), allocated for every set.
@@ -1228,6 +1301,14 @@ void launch_finish_v(mrt_ctx* c, int qi, uint32_t cur, const RenderParams& rp, b
   HIP_CHECK(hipGetLastError());
 }
 
+// Work enqueued on a caller's stream `st` that writes the context's shared
+// buffers (q[0].ctrl, the results slab, the lane-ray slots): the next
+// wavefront render forks its queues after acc_done[s], so recording every
+// set's acc_done here orders that render after this work too.
+void mark_ctx_busy(mrt_ctx* c, hipStream_t st) {
+  for (int s = 0; s < c->n_sets; ++s) HIP_CHECK(hipEventRecord(c->acc_done[s], st));
+}
+
 // The fused path loop: one k_render launch + one k_accumulate per chunk.
 void render_fused(mrt_ctx* c, const mrt_render_args* a, const uint32_t* pixlist_d, uint32_t n_pix, uint32_t spp_chunk,
                   float* d_rgb, uint32_t* d_b, hipStream_t st) {
@@ -1268,7 +1349,13 @@ void render_fused(mrt_ctx* c, const mrt_render_args* a, const uint32_t* pixlist_
                        n_pix, cs, pixlist_d, d_rgb, d_b);
     HIP_CHECK(hipGetLastError());
   }
+  mark_ctx_busy(c, st);
 }
+
+void resolve_kernel_timing(mrt_ctx* c);
+// pending kernel-timing marks resolved at the start of a timed render once
+// this many accumulated (a caller that never reads the stats)
+constexpr size_t kMaxPendingMarks = 1u << 14;
 
 void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t* d_b, hipStream_t st) {
   if (!a) throw ApiError{MRT_ERR_INVALID, "null render args"};
@@ -1301,6 +1388,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
   ensure_results(c, (size_t)n_pix * spp_chunk);
   const int K = c->n_queues;
   const bool timing = (a->flags & MRT_RENDER_TIME_KERNELS) != 0;
+  if (timing && c->pend_marks.size() + c->pend_fin.size() > kMaxPendingMarks) resolve_kernel_timing(c);
   // the drain hand-off (launch_finish_v): the fused kernel has no traversal
   // draws or composite surfaces; its lane-ray slots are allocated here, before
   // any queue runs (ensure_slots reallocates)
@@ -1363,7 +1451,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
       }
       base += nk;
     }
-    const uint32_t grid = (uint32_t)((c->q[0].cap + kBlock - 1) / kBlock);
+    const uint32_t grid = shade_grid(c, count);
     std::vector<std::array<hipEvent_t, 3>> marks;
     std::vector<std::array<hipEvent_t, 2>> fin_marks;
     const int kBatch = 4;  // even: a status read sees the live pool in active[0]
@@ -1577,12 +1665,17 @@ int mrt_create(int device, mrt_ctx** out) {
 
 }  // extern "C"
 
-int massrt_ctx_device(const mrt_ctx* c) { return c ? c->device : -1; }
+int massrt_ctx_device(const mrt_ctx* c) { return c ? c->device : -1; }  // device 0's for a multi-device context
 
 extern "C" {
 
 int mrt_destroy(mrt_ctx* c) {
   if (!c) return MRT_OK;
+  if (c->multi) {
+    multi_free(c->multi);
+    delete c;
+    return MRT_OK;
+  }
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   for (Queue& q : c->q)
@@ -1622,6 +1715,7 @@ int mrt_destroy(mrt_ctx* c) {
 }
 
 int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
+  MRT_EACH(c, mrt_upload_scene(c, d));
   return guarded(c, [&] {
     if (!d) throw ApiError{MRT_ERR_INVALID, "null scene"};
     HostScene hs;
@@ -1736,6 +1830,7 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
 }
 
 int mrt_scene_device_bytes(mrt_ctx* c, uint64_t* out) {
+  MRT_DEV0(c, mrt_scene_device_bytes(c, out));
   return guarded(c, [&] {
     if (!out) throw ApiError{MRT_ERR_INVALID, "null output"};
     *out = c->scene_bytes;
@@ -1743,6 +1838,7 @@ int mrt_scene_device_bytes(mrt_ctx* c, uint64_t* out) {
 }
 
 int mrt_set_camera(mrt_ctx* c, const mrt_camera* cam) {
+  MRT_EACH(c, mrt_set_camera(c, cam));
   return guarded(c, [&] {
     if (!cam) throw ApiError{MRT_ERR_INVALID, "null camera"};
     DevCamera d;
@@ -1759,6 +1855,7 @@ int mrt_set_camera(mrt_ctx* c, const mrt_camera* cam) {
 }
 
 int mrt_render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t* d_b, void* stream) {
+  MRT_DEV0(c, mrt_render_device(c, a, d_rgb, d_b, stream));
   return guarded(c, [&] {
     if (!d_rgb || !d_b) throw ApiError{MRT_ERR_INVALID, "null accumulation buffer"};
     render_device(c, a, d_rgb, d_b, (hipStream_t)stream);  // NULL: the null stream
@@ -1766,6 +1863,7 @@ int mrt_render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32
 }
 
 int mrt_render(mrt_ctx* c, const mrt_render_args* a, float* rgb, uint32_t* bounces) {
+  if (c && c->multi) return multi_render(c->multi, a, rgb, bounces, c->err);
   return guarded(c, [&] {
     if (!a || !rgb || !bounces) throw ApiError{MRT_ERR_INVALID, "null argument"};
     size_t np = (size_t)a->width * a->height;
@@ -1788,6 +1886,7 @@ int mrt_render(mrt_ctx* c, const mrt_render_args* a, float* rgb, uint32_t* bounc
 }
 
 int mrt_trace_rays(mrt_ctx* c, const float* rays, uint32_t n, float t_min, float t_max, mrt_hit* out) {
+  MRT_DEV0(c, mrt_trace_rays(c, rays, n, t_min, t_max, out));
   return guarded(c, [&] {
     if (!c->has_scene) throw ApiError{MRT_ERR_STATE, "no scene uploaded"};
     if (n == 0) return;
@@ -1828,6 +1927,19 @@ int mrt_trace_rays(mrt_ctx* c, const float* rays, uint32_t n, float t_min, float
 }
 
 int mrt_get_counters(mrt_ctx* c, mrt_counters* out) {
+  if (c && c->multi && out) {  // summed over the devices
+    mrt_counters sum{};
+    const int rc = on_each(c, [&](mrt_ctx* d) {
+      mrt_counters x{};
+      const int r = mrt_get_counters(d, &x);
+      const uint64_t* px = reinterpret_cast<const uint64_t*>(&x);
+      uint64_t* ps = reinterpret_cast<uint64_t*>(&sum);
+      for (size_t k = 0; k < sizeof(x) / 8; ++k) ps[k] += px[k];
+      return r;
+    });
+    *out = sum;
+    return rc;
+  }
   return guarded(c, [&] {
     if (!out) throw ApiError{MRT_ERR_INVALID, "null output"};
     HIP_CHECK(hipStreamSynchronize(c->stream));
@@ -1847,10 +1959,24 @@ int mrt_get_counters(mrt_ctx* c, mrt_counters* out) {
     out->wave_slots = h.wave_slots;
     out->lane_steps = h.lane_steps;
     out->box_exact = h.box_exact;
+    out->shaded = h.shaded;
   });
 }
 
 int mrt_get_kernel_stats(mrt_ctx* c, mrt_kernel_stats* out) {
+  if (c && c->multi && out) {  // summed over the devices
+    mrt_kernel_stats sum{};
+    const int rc = on_each(c, [&](mrt_ctx* d) {
+      mrt_kernel_stats x{};
+      const int r = mrt_get_kernel_stats(d, &x);
+      sum.trace_ms += x.trace_ms, sum.shade_ms += x.shade_ms, sum.other_ms += x.other_ms;
+      sum.trace_launches += x.trace_launches, sum.shade_launches += x.shade_launches;
+      sum.iterations += x.iterations, sum.finish_ms += x.finish_ms, sum.finish_launches += x.finish_launches;
+      return r;
+    });
+    *out = sum;
+    return rc;
+  }
   return guarded(c, [&] {
     if (!out) throw ApiError{MRT_ERR_INVALID, "null output"};
     resolve_kernel_timing(c);
@@ -1859,6 +1985,7 @@ int mrt_get_kernel_stats(mrt_ctx* c, mrt_kernel_stats* out) {
 }
 
 int mrt_reset_kernel_stats(mrt_ctx* c) {
+  MRT_EACH(c, mrt_reset_kernel_stats(c));
   return guarded(c, [&] {
     resolve_kernel_timing(c);
     c->kstats = mrt_kernel_stats{};
@@ -1866,6 +1993,7 @@ int mrt_reset_kernel_stats(mrt_ctx* c) {
 }
 
 int mrt_selftest_division(mrt_ctx* c, uint64_t n, uint64_t seed, uint64_t* mismatches) {
+  MRT_DEV0(c, mrt_selftest_division(c, n, seed, mismatches));
   return guarded(c, [&] {
     if (!mismatches) throw ApiError{MRT_ERR_INVALID, "null output"};
     unsigned long long* d = nullptr;
@@ -1884,6 +2012,7 @@ int mrt_selftest_division(mrt_ctx* c, uint64_t n, uint64_t seed, uint64_t* misma
 
 int mrt_tonemap_device(mrt_ctx* c, uint32_t W, uint32_t H, const float* d_rgb, const uint32_t* d_b, uint32_t passes,
                        uint32_t mode, uint8_t* d_out, void* stream) {
+  MRT_DEV0(c, mrt_tonemap_device(c, W, H, d_rgb, d_b, passes, mode, d_out, stream));
   return guarded(c, [&] {
     if (W == 0 || H == 0 || (uint64_t)W * H >= (1ull << 32)) throw ApiError{MRT_ERR_INVALID, "bad image size"};
     if (mode > MRT_DISPLAY_NORMAL) throw ApiError{MRT_ERR_INVALID, "bad display mode"};
@@ -1911,6 +2040,7 @@ int mrt_tonemap_device(mrt_ctx* c, uint32_t W, uint32_t H, const float* d_rgb, c
 
 int mrt_tonemap(mrt_ctx* c, uint32_t W, uint32_t H, const float* rgb, const uint32_t* b, uint32_t passes,
                 uint32_t mode, uint8_t* out) {
+  MRT_DEV0(c, mrt_tonemap(c, W, H, rgb, b, passes, mode, out));
   return guarded(c, [&] {
     if (W == 0 || H == 0 || (uint64_t)W * H >= (1ull << 32)) throw ApiError{MRT_ERR_INVALID, "bad image size"};
     if (!out || !rgb || !b) throw ApiError{MRT_ERR_INVALID, "null buffer"};
@@ -1935,6 +2065,7 @@ int mrt_tonemap(mrt_ctx* c, uint32_t W, uint32_t H, const float* rgb, const uint
 
 int mrt_prepass_device(mrt_ctx* c, uint32_t W, uint32_t H, uint64_t seed, float* d_albedo, float* d_normal,
                        void* stream) {
+  MRT_DEV0(c, mrt_prepass_device(c, W, H, seed, d_albedo, d_normal, stream));
   return guarded(c, [&] {
     if (!c->has_scene) throw ApiError{MRT_ERR_STATE, "no scene uploaded"};
     if (!c->has_camera) throw ApiError{MRT_ERR_STATE, "no camera set"};
@@ -1949,10 +2080,12 @@ int mrt_prepass_device(mrt_ctx* c, uint32_t W, uint32_t H, uint64_t seed, float*
     hipLaunchKernelGGL(prepass, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c->S, c->cam, W, H,
                        (unsigned long long)seed, c->slot_ro, c->slot_rd, d_albedo, d_normal);
     HIP_CHECK(hipGetLastError());
+    mark_ctx_busy(c, st);  // the pre-pass rays live in slot_ro/slot_rd, which the drain hand-off reuses
   });
 }
 
 int mrt_prepass(mrt_ctx* c, uint32_t W, uint32_t H, uint64_t seed, float* albedo, float* normal) {
+  MRT_DEV0(c, mrt_prepass(c, W, H, seed, albedo, normal));
   return guarded(c, [&] {
     if (W == 0 || H == 0 || (uint64_t)W * H >= (1ull << 32)) throw ApiError{MRT_ERR_INVALID, "bad image size"};
     if (!albedo || !normal) throw ApiError{MRT_ERR_INVALID, "null buffer"};
@@ -1972,6 +2105,7 @@ int mrt_prepass(mrt_ctx* c, uint32_t W, uint32_t H, uint64_t seed, float* albedo
 }
 
 int mrt_selftest_slab(mrt_ctx* c, uint64_t n, uint64_t seed, uint64_t* mismatches, uint64_t* near_ties) {
+  MRT_DEV0(c, mrt_selftest_slab(c, n, seed, mismatches, near_ties));
   return guarded(c, [&] {
     if (!mismatches || !near_ties) throw ApiError{MRT_ERR_INVALID, "null output"};
     unsigned long long* d = nullptr;
@@ -1990,6 +2124,7 @@ int mrt_selftest_slab(mrt_ctx* c, uint64_t n, uint64_t seed, uint64_t* mismatche
 }
 
 int mrt_debug_status(mrt_ctx* c, uint32_t* out4) {
+  MRT_DEV0(c, mrt_debug_status(c, out4));
   return guarded(c, [&] {
     if (!out4) throw ApiError{MRT_ERR_INVALID, "null output"};
     HIP_CHECK(hipDeviceSynchronize());
@@ -2049,15 +2184,18 @@ static int shard_exchange(mrt_ctx* c, uint32_t W, uint32_t H, uint32_t si, uint3
 
 int mrt_shard_pack_device(mrt_ctx* c, uint32_t W, uint32_t H, uint32_t si, uint32_t sc, const float* d_rgb,
                           const uint32_t* d_b, void* d_slab, void* stream) {
+  MRT_DEV0(c, mrt_shard_pack_device(c, W, H, si, sc, d_rgb, d_b, d_slab, stream));
   return shard_exchange(c, W, H, si, sc, d_rgb, d_b, d_slab, nullptr, nullptr, stream, true);
 }
 
 int mrt_shard_unpack_device(mrt_ctx* c, uint32_t W, uint32_t H, uint32_t si, uint32_t sc, const void* d_slab,
                             float* d_rgb, uint32_t* d_b, void* stream) {
+  MRT_DEV0(c, mrt_shard_unpack_device(c, W, H, si, sc, d_slab, d_rgb, d_b, stream));
   return shard_exchange(c, W, H, si, sc, nullptr, nullptr, d_slab, d_rgb, d_b, stream, false);
 }
 
 int mrt_reset_counters(mrt_ctx* c) {
+  MRT_EACH(c, mrt_reset_counters(c));
   return guarded(c, [&] {
     HIP_CHECK(hipDeviceSynchronize());
     HIP_CHECK(hipMemset(c->d_cnt, 0, sizeof(DevCounters)));

@@ -26,7 +26,7 @@ LIB_PATH = (Path(_SEL) if _SEL.endswith(".so") else
 REPO = _HERE.parent.parent
 
 # ---- constants (massrt.h) --------------------------------------------------
-ABI_VERSION = 6  # MRT_ABI_VERSION this binding was written for
+ABI_VERSION = 7  # MRT_ABI_VERSION this binding was written for
 REF_NONE, REF_NODE, REF_SPHERE, REF_TRIANGLE, REF_INSTANCE, REF_MODEL, REF_VOLUME = range(7)
 MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_SPECULAR, MAT_ISOTROPHIC, MAT_MIX = range(8)
 WRAP_MIRROR, WRAP_REPEAT, WRAP_CLAMP = range(3)
@@ -148,7 +148,7 @@ class MrtKernelStats(C.Structure):
 
 
 # scheduling counters of the persistent k_trace (no reference counterpart)
-SCHED_FIELDS = ["wave_slots", "lane_steps", "box_exact"]
+SCHED_FIELDS = ["wave_slots", "lane_steps", "box_exact", "shaded"]
 
 
 class MrtCounters(C.Structure):
@@ -175,6 +175,9 @@ EXPORTED_SYMBOLS = [
     "mrt_tonemap_device", "mrt_tonemap", "mrt_write_png", "mrt_display_gamma_thresholds",
     "mrt_prepass_device", "mrt_prepass",
     "mrt_shard_pixels", "mrt_shard_pack_device", "mrt_shard_unpack_device",
+    "mrt_create_multi", "mrt_context_devices", "mrt_image_create", "mrt_image_destroy", "mrt_image_clear",
+    "mrt_image_render", "mrt_image_prepass", "mrt_image_read", "mrt_image_tonemap", "mrt_image_gather_stats",
+    "mrt_build_info",
 ]
 
 _lib = None
@@ -249,6 +252,17 @@ def lib() -> C.CDLL:
         "mrt_shard_pixels": (I, [U32, U32, U32, U32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
         "mrt_shard_pack_device": (I, [P, U32, U32, U32, U32, P, P, P, P]),
         "mrt_shard_unpack_device": (I, [P, U32, U32, U32, U32, P, P, P, P]),
+        "mrt_create_multi": (I, [I, C.POINTER(C.c_int), C.POINTER(P)]),
+        "mrt_context_devices": (I, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+        "mrt_image_create": (I, [P, U32, U32, C.POINTER(P)]),
+        "mrt_image_destroy": (I, [P]),
+        "mrt_image_clear": (I, [P]),
+        "mrt_image_render": (I, [P, U64, U32, U32, U32, U32]),
+        "mrt_image_prepass": (I, [P, U64]),
+        "mrt_image_read": (I, [P, fp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+        "mrt_image_tonemap": (I, [P, U32, C.POINTER(C.c_uint8)]),
+        "mrt_image_gather_stats": (I, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
+        "mrt_build_info": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -444,15 +458,34 @@ def preorder(desc: MrtSceneDesc):
     return out, boxes
 
 
-class Context:
-    """One GPU context (mrt_ctx). Raises if no HIP device is present."""
+def build_info() -> str:
+    """"src <hash>": the source hash the loaded library was built from (tools/src_hash.py)."""
+    return lib().mrt_build_info().decode()
 
-    def __init__(self, device: int = 0):
+
+class Context:
+    """One GPU context (mrt_ctx), or one over several devices (devices=[...],
+    mrt_create_multi). Raises if no HIP device is present."""
+
+    def __init__(self, device: int = 0, devices=None):
         h = C.c_void_p()
-        rc = lib().mrt_create(device, C.byref(h))
+        if devices is not None:
+            ids = (C.c_int * len(devices))(*devices)
+            rc = lib().mrt_create_multi(len(devices), ids, C.byref(h))
+            what = "mrt_create_multi"
+        else:
+            rc = lib().mrt_create(device, C.byref(h))
+            what = "mrt_create"
         if rc != 0:
-            raise MassrtError(f"mrt_create failed ({rc}): {lib().mrt_global_last_error().decode()}")
+            raise MassrtError(f"{what} failed ({rc}): {lib().mrt_global_last_error().decode()}")
         self.h = h
+
+    def devices(self) -> list:
+        n = C.c_int()
+        self._check(lib().mrt_context_devices(self.h, C.byref(n), None))
+        ids = (C.c_int * n.value)()
+        self._check(lib().mrt_context_devices(self.h, C.byref(n), ids))
+        return list(ids)
 
     def _check(self, rc):
         if rc != 0:
@@ -638,3 +671,127 @@ def load_obj(path) -> np.ndarray:
     out = np.zeros((n, 24), dtype=np.float32)
     lib().mrt_load_obj(str(path).encode(), _fptr(out), n)
     return out
+
+
+class Image:
+    """The reference's Image (main.rs:598-638) in HBM (mrt_image): colour and
+    depth sums plus the pass count stay on the context's device(s); render()
+    adds passes without a host round trip, read()/tonemap() cross PCIe."""
+
+    def __init__(self, ctx: Context, width: int, height: int):
+        h = C.c_void_p()
+        rc = lib().mrt_image_create(ctx.h, width, height, C.byref(h))
+        if rc != 0:
+            raise MassrtError(lib().mrt_last_error(ctx.h).decode())
+        self.h, self.ctx, self.width, self.height = h, ctx, width, height
+
+    def _check(self, rc):
+        if rc != 0:
+            raise MassrtError(lib().mrt_last_error(self.ctx.h).decode())
+
+    def close(self):
+        if self.h:
+            lib().mrt_image_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def clear(self):
+        """Image::clear (main.rs:749-758)."""
+        self._check(lib().mrt_image_clear(self.h))
+
+    def render(self, seed: int, spp_begin: int, passes: int, max_depth: int = MAX_DEPTH, counters=False,
+               time_kernels=False):
+        """`passes` 1-spp passes merged: samples [spp_begin, spp_begin + passes) of every pixel."""
+        flags = (RENDER_COUNTERS if counters else 0) | (RENDER_TIME_KERNELS if time_kernels else 0)
+        self._check(lib().mrt_image_render(self.h, seed, spp_begin, passes, max_depth, flags))
+
+    def prepass(self, seed: int = 1):
+        """Camera::albedo_normal pre-pass into the image (main.rs:162-222)."""
+        self._check(lib().mrt_image_prepass(self.h, seed))
+
+    @property
+    def passes(self) -> int:
+        p = C.c_uint32()
+        self._check(lib().mrt_image_read(self.h, None, None, C.byref(p)))
+        return int(p.value)
+
+    def read(self):
+        """(rgb float32 [H*W*3], bounces uint32 [H*W], passes)."""
+        n = self.width * self.height
+        rgb = np.empty(3 * n, dtype=np.float32)
+        b = np.empty(n, dtype=np.uint32)
+        p = C.c_uint32()
+        self._check(lib().mrt_image_read(self.h, _fptr(rgb), b.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(p)))
+        return rgb, b, int(p.value)
+
+    def tonemap(self, mode: int = 0) -> np.ndarray:
+        """Image::to_rgb_bytes + dump's row flip: (H, W, 3) uint8, top row first."""
+        out = np.empty(self.width * self.height * 3, dtype=np.uint8)
+        self._check(lib().mrt_image_tonemap(self.h, mode, out.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return out.reshape(self.height, self.width, 3)
+
+    def gather_stats(self):
+        """(bytes moved between devices by this image's gathers, their wall ms)."""
+        b, ms = C.c_uint64(), C.c_double()
+        self._check(lib().mrt_image_gather_stats(self.h, C.byref(b), C.byref(ms)))
+        return int(b.value), float(ms.value)
+
+
+# ---- render(): the drop-in pass loop (mirror of bindings/rust/src/lib.rs) ---
+
+class SampleStreams:
+    """Where a frame's samples come from (lib.rs SampleStreams). The
+    reference's render threads draw from thread-local fastrand streams seeded
+    afresh for every render() call (main.rs:167-250), so frames never share
+    samples; here sample s of pixel p is keyed (seed, p, s) and the sample
+    index keeps counting across frames (the seed moves on before it wraps)."""
+
+    def __init__(self, seed: int = 1, next_sample: int = 0):
+        self.seed, self.next_sample = seed, next_sample
+
+    def take(self, n: int):
+        if self.next_sample + n > 0xFFFFFFFF:
+            self.seed = (self.seed + 1) & 0xFFFFFFFFFFFFFFFF
+            self.next_sample = 0
+        first = self.next_sample
+        self.next_sample += n
+        return self.seed, first
+
+
+def default_workers() -> int:
+    """render()'s thread count: num_cpus - 2, at least 1 (main.rs:159-160)."""
+    return max(1, (os.cpu_count() or 1) - 2)
+
+
+def render(image, streams: SampleStreams, frame_limit=None, workers=None, batch=64, max_depth=MAX_DEPTH,
+           prepass=True, update=None, keep_going=None) -> int:
+    """render(image, event_proxy, world, camera, frame_limit) (main.rs:150-295)
+    on the GPU, exactly as bindings/rust/src/lib.rs `render` does it:
+    pre-pass (main.rs:162-222), Image::clear (main.rs:233), then `workers`
+    render threads x `frame_limit` whole 1-spp passes each (None: until
+    keep_going() is false), one merge per pass (main.rs:243-280), run `batch`
+    passes per mrt_image_render call; update(image, passes) after every batch
+    (UserEvent::Update, main.rs:274-278); keep_going() before every batch
+    (QUICK_PASS, main.rs:224-231, 282-284). Returns the passes rendered."""
+    workers = default_workers() if workers is None else max(1, int(workers))
+    if prepass:
+        image.prepass(streams.seed)
+    image.clear()
+    total = None if frame_limit is None else int(frame_limit) * workers
+    batch = max(1, int(batch))
+    done = 0
+    while total is None or done < total:
+        if keep_going is not None and not keep_going():
+            break
+        k = batch if total is None else min(batch, total - done)
+        seed, first = streams.take(k)
+        image.render(seed, first, k, max_depth)
+        done += k
+        if update is not None:
+            update(image, image.passes)
+    return done

@@ -43,6 +43,7 @@ class ShardedFrame:
         self.rgb = torch.zeros(width * height * 3, dtype=torch.float32, device=device)
         self.bounces = torch.zeros(width * height, dtype=torch.int32, device=device)
         self.spp = 0
+        self._marks = []  # (start, end) CUDA events around each publish on a GPU
         if world == 1:
             self.out_rgb, self.out_bounces = self.rgb, self.bounces
             return
@@ -97,6 +98,10 @@ class ShardedFrame:
         """Gather every rank's tile slab onto rank 0 (no-op for one rank)."""
         if self.world == 1:
             return
+        timed = self.rgb.is_cuda
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         self._pack()
         if self.slab.is_cuda and dist.get_backend() == "gloo":  # gloo gathers host tensors (rehearsal/tests)
             torch.cuda.current_stream().synchronize()
@@ -110,6 +115,21 @@ class ShardedFrame:
         if self.rank == 0:
             for r, s in enumerate(self.slabs):
                 self._unpack(r, s)
+        if timed:
+            e1.record()
+            self._marks.append((e0, e1))
+
+    def gather_ms(self, reset: bool = True) -> float:
+        """Milliseconds the publishes since the last reset took on this rank's
+        stream (pack + gather + unpack; a rank's gather includes waiting for
+        the slowest rank)."""
+        if not self._marks:
+            return 0.0
+        self._marks[-1][1].synchronize()
+        t = sum(a.elapsed_time(b) for a, b in self._marks)
+        if reset:
+            self._marks = []
+        return t
 
     def frame(self):
         """(rgb, bounces) of the whole image — valid on rank 0 after publish()."""

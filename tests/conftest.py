@@ -22,6 +22,22 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: builds the 1M-triangle scenes")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first(request):
+    """In one process torch must initialise HIP before libmassrt does: torch
+    ships its own HIP runtime, and once libmassrt's (/opt/rocm) has opened the
+    device torch's init reports "No HIP GPUs are available" (measured on the
+    MI355X box with this round's and round 2's library alike,
+    tools/diag/torch_after_raw.py). bench.py and the multi-rank tests set the
+    torch device first; the GPU test session does it here."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        import torch
+
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    yield
+
+
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN

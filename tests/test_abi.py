@@ -24,7 +24,7 @@ def test_header_symbols_exported():
 
 
 def test_abi_version():
-    assert massrt.lib().mrt_abi_version() == massrt.ABI_VERSION == 6
+    assert massrt.lib().mrt_abi_version() == massrt.ABI_VERSION == 7
 
 
 def test_struct_layouts_match_header(tmp_path):
@@ -58,6 +58,22 @@ def test_struct_layouts_match_header(tmp_path):
         else:
             cname, f = key.split(".")
             assert getattr(structs[cname], f).offset == int(val), key
+
+
+def test_library_was_built_from_this_tree():
+    """mrt_build_info carries the source hash the Makefile baked in: the
+    library the tests (and the GPU box) load is HEAD's code, not a stale build."""
+    import src_hash
+
+    assert massrt.build_info() == "src " + src_hash.src_hash()
+
+
+def test_no_gpu_multi_device_context_fails_loudly():
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(massrt.MassrtError, match="no HIP device"):
+        massrt.Context(devices=[0, 0])
 
 
 def test_no_gpu_fails_loudly():
