@@ -315,9 +315,9 @@ def load_pmc(path: Path, stamp: dict):
     return pj
 
 
-def limiter(pj: dict):
-    """Utilisation of the units k_trace can be bound by, from the PMC summary."""
-    k = pj.get("kernels", {}).get("k_trace", {})
+def limiter(pj: dict, kernel: str = "k_trace"):
+    """Utilisation of the units `kernel` can be bound by, from the PMC summary."""
+    k = pj.get("kernels", {}).get(kernel, {})
     out = {}
     avg_ns = k.get("avg_ns")
     if k.get("hbm_bytes_per_launch") and avg_ns:
@@ -438,7 +438,7 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
         }
 
     shade = None
-    if timing and cnt.get("shaded") and ks["shade_launches"] > 0:
+    if timing and cnt.get("shaded") and ks["shade_launches"] > 0 and roof is not None:
         # k_shade: HBM-streaming (path state in and out), SHADE_BYTES per shaded path
         shaded = cnt["shaded"] / max(cnt["samples"], 1) * (samples_total / world)
         sb = SHADE_BYTES * shaded / ks["shade_launches"]
@@ -447,6 +447,11 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
                  "launches": int(ks["shade_launches"]), "achieved": round(sb / (sms * 1e-3) / 1e9, 1),
                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(sb / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                  "bytes_per_path": SHADE_BYTES, "paths_per_sample": round(cnt["shaded"] / max(cnt["samples"], 1), 4)}
+        ksh = pj["kernels"].get("k_shade", {}) if pj else {}
+        if ksh.get("hbm_bytes_per_launch"):  # PMC of the same source and config (rocprof's per-launch average)
+            shade["traffic"] = round(ksh["hbm_bytes_per_launch"])
+            shade["pmc_avg_launch_ms"] = round(ksh["avg_ns"] * 1e-6, 4)
+            shade["limiter"] = {k: round(v, 4) for k, v in limiter(pj, "k_shade").items()}
     out = {"scene": scene, "value": round(value, 3), "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps,
            "warmup": warmup, "width": W, "height": H, "spp_per_step": spp, "samples_per_step": W * H * spp,
            "scene_load_s": round(t_load, 2), "roofline": roof, "roofline_k_shade": shade}

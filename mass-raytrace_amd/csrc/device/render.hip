@@ -54,7 +54,8 @@ constexpr uint32_t kGroups = 8;
 struct Ctrl {
   uint32_t active[2];
   uint32_t next_work;
-  uint32_t pad_[29];
+  uint32_t shade_short;  // nonzero: a k_shade grid did not cover its live pool (host bound wrong; reported)
+  uint32_t pad_[28];
   // persistent k_trace work counters (zeroed by k_shade), one 128-B line per
   // XCD group: group g takes its rays from the g-th eighth of the pool
   uint32_t group_next[kGroups * 32];
@@ -399,14 +400,19 @@ __global__ __launch_bounds__(kBlock, MRT_SHADE_WPE) void k_shade(DevScene S, Dev
                                                   uint32_t* work, float4* results, DevCounters* cnt) {
   const uint32_t n = ctrl->active[cur];
   if (blockIdx.x == 0 && threadIdx.x < kGroups) ctrl->group_next[threadIdx.x * 32] = 0;  // next k_trace
+  // one workgroup per 256 live paths: the host sizes the grid from a bound on
+  // the live count (shade_grid), so a drain launch does not dispatch a
+  // workgroup per 256 slots of the whole pool. A bound that fell short is
+  // reported to the host, never dropped silently. (A grid-stride loop here
+  // made the kernel spill 80 B instead of 44 and cost 3.5% of the frame.)
+  if (blockIdx.x == 0 && threadIdx.x == 0 && n > gridDim.x * kBlock) ctrl->shade_short = n;
   LocalCounters lc;
   uint32_t nbounce = 0, nsample = 0, nshaded = 0;
   __shared__ uint32_t s_cnt[kWaves], s_base;
   const uint32_t wave = threadIdx.x / 64;
-  // grid-stride over the live pool: the grid is sized to the GPU, not to the
-  // pool's capacity, so a drain launch with few live paths does not dispatch
-  // (and retire) a workgroup per 256 slots of a 64M-slot pool
-  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {  // uniform per workgroup
+  {
+    const uint32_t base = blockIdx.x * kBlock;
+    if (base >= n) return;
     const uint32_t i = base + threadIdx.x;
     bool alive = false, need = false;
     float4 ro{}, rd{}, thr{}, rad{};
@@ -1154,26 +1160,15 @@ void launch_trace(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in
   HIP_CHECK(hipGetLastError());
 }
 
-// k_shade's grid: it strides over the live pool, so enough workgroups to
-// fill every CU at its occupancy (MRT_SHADE_WGS_PER_CU overrides), never
-// more than the pool's capacity needs.
-uint32_t shade_grid(mrt_ctx* c, bool count) {
-  const void* f = count ? (c->scene_ext ? (const void*)k_shade<true, true> : (const void*)k_shade<true, false>)
-                        : (c->scene_ext ? (const void*)k_shade<false, true> : (const void*)k_shade<false, false>);
-  auto key = std::make_pair(f, (size_t)1);  // (kernel, tag) in the persistent-grid cache
-  auto it = c->grids.find(key);
-  uint32_t g = 0;
-  if (it != c->grids.end()) {
-    g = it->second;
-  } else {
-    int per_cu = 0;
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, 0));
-    if (const char* e = getenv("MRT_SHADE_WGS_PER_CU")) per_cu = atoi(e);
-    g = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
-    c->grids[key] = g;
-  }
-  const uint32_t need = (uint32_t)((c->q[0].cap + kBlock - 1) / kBlock);
-  return std::max<uint32_t>(1, std::min(g, need));
+// k_shade's grid for a pool known to hold at most `bound` live paths: one
+// workgroup per 256 of them.
+// While the work counter has items left the pool refills to capacity; once
+// it is exhausted the live count only falls, so the last status the host
+// read bounds every later launch — a drain launch then dispatches a few
+// workgroups instead of one per 256 slots of the whole pool.
+uint32_t shade_grid(const Queue& q, size_t bound) {
+  const size_t n = std::min(q.cap, bound);
+  return (uint32_t)std::max<size_t>(1, (n + kBlock - 1) / kBlock);
 }
 
 // P paths per queue set (n_queues queues), allocated for every set.
@@ -1451,7 +1446,6 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
       }
       base += nk;
     }
-    const uint32_t grid = shade_grid(c, count);
     std::vector<std::array<hipEvent_t, 3>> marks;
     std::vector<std::array<hipEvent_t, 2>> fin_marks;
     const int kBatch = 4;  // even: a status read sees the live pool in active[0]
@@ -1459,6 +1453,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
       uint32_t it = 0;
       int slot = 0;
       bool pending = false, finished = false;
+      size_t bound = ~(size_t)0;  // live paths at most (shade_grid)
     } st_[kMaxQueues];
     int open = K;
     while (open > 0) {
@@ -1490,7 +1485,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
           {
             auto* shade = count ? (c->scene_ext ? k_shade<true, true> : k_shade<true, false>)
                                 : (c->scene_ext ? k_shade<false, true> : k_shade<false, false>);
-            hipLaunchKernelGGL(shade, dim3(grid), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, q.bufs[cur],
+            hipLaunchKernelGGL(shade, dim3(shade_grid(q, L.bound)), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, q.bufs[cur],
                                q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, work, res, c->d_cnt);
           }
           HIP_CHECK(hipGetLastError());
@@ -1506,6 +1501,10 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
         if (L.pending) {  // the previous batch's status (one batch stays in flight)
           HIP_CHECK(hipEventSynchronize(q.ev[L.slot ^ 1]));
           const Ctrl& s = q.h_status[L.slot ^ 1];
+          if (s.shade_short)
+            throw ApiError{MRT_ERR_HIP, "internal: a k_shade grid was smaller than its live pool (" +
+                                            std::to_string(s.shade_short) + " paths)"};
+          if (q.h_work[L.slot ^ 1] >= rp.G) L.bound = std::min<size_t>(L.bound, s.active[0]);
           if (q.h_work[L.slot ^ 1] >= rp.G && s.active[0] <= finish_paths) {
             // no new work: the paths left (at most as many as that status
             // showed) finish in one fused launch after the batch just queued

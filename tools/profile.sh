@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 SCENE=${SCENE:-sphere_grid}
 OUT=gpurun_out/prof_$SCENE
 rm -rf $OUT; mkdir -p $OUT
-B="bench.py --scene $SCENE --no-cpu-baseline --secondary none"
+B="bench.py --scene $SCENE --no-cpu-baseline --no-dropin --secondary none"
 P="--steps 1 --warmup 1 --no-kernel-timing"
 run() {  # name, timeout, rocprofv3 args...
   local name=$1 t=$2; shift 2
