@@ -14,15 +14,19 @@
 //
 // Records are made of 16-byte slots (uint4); the kind is slot1.w, and a box
 // says it is one by bit 31 there (kBoxFlag), the rest of that word being the
-// index its box-hit step goes to (its first child: the next record of the
-// plain stream):
+// index its box-hit step goes to (its first child). Boxes, spheres, triangles
+// and volumes name their successors explicitly (hit / skip / next), so a
+// region's records may sit in any order (round 3: BLAS regions are laid out
+// with siblings together, upload.cpp relayout_blas); instances and models
+// return to the record right after them:
 //   BOX    2 slots  {min.x,min.y,min.z,max.x} {max.y,max.z,skip,kBoxFlag|hit}
-//   SPHERE 2 slots  {cx,cy,cz,r}              {sphere_id,0,0,SPHERE}
-//   TRI    3 slots  {a.x,a.y,a.z,ab.x}        {ab.y,ab.z,tri_id,TRI} {ac.x,ac.y,ac.z,flags}
+//   SPHERE 2 slots  {cx,cy,cz,r}              {sphere_id,next,0,SPHERE}
+//   TRI    3 slots  {a.x,a.y,a.z,ab.x}        {ab.y,ab.z,tri_id|alpha,TRI} {ac.x,ac.y,ac.z,next}
 //   INST   2 slots  {inst_id,blas_begin,blas_end,0} {0,0,0,INST}
 //   MODEL  2 slots  {model_id,blas_begin,blas_end,0} {0,0,0,MODEL}
-//   VOLUME 2 slots  {cx,cy,cz,r}              {volume_id,0,0,VOLUME}  (sphere target)
+//   VOLUME 2 slots  {cx,cy,cz,r}              {volume_id,next,0,VOLUME}  (sphere target)
 //   END    2 slots  {0,0,0,0}                 {0,0,0,END}   closes every region
+// Slots between records (alignment padding) are zero and never reached.
 // ab = b - a and ac = c - a are precomputed on the host with the same IEEE
 // subtraction Triangle::intersect performs (geom.rs:505-506).
 #pragma once
@@ -43,7 +47,10 @@ constexpr uint32_t kLdsTag = 0x40000000u;
 constexpr uint32_t kIdxMask = 0x3FFFFFFFu;
 // the region being traversed has ended (record after its last one; path.h)
 constexpr uint32_t KIND_END = 0;
-enum : uint32_t { TRI_FLAG_ALPHA = 1u, TRI_FLAG_UV = 2u };
+enum : uint32_t { TRI_FLAG_ALPHA = 1u, TRI_FLAG_UV = 2u };  // tri_shade flags
+// a TRI record's slot1.z: the triangle id, bit 31 = the triangle is alpha-tested
+constexpr uint32_t kTriAlpha = 0x80000000u;
+constexpr uint32_t kTriIdMask = 0x0FFFFFFFu;
 
 // Composite surfaces (YCbCrTexture, TextureBlend, SolidColorFallback,
 // texture.rs:197-357) run as small postfix programs over a V4 stack:

@@ -56,6 +56,10 @@ MRT_DEV uint32_t mrt_chk(uint32_t* dbg, uint32_t idx, uint32_t bound, uint32_t c
 
 MRT_DEV float u2f(uint32_t u) { return __uint_as_float(u); }
 MRT_DEV V3 ld3(const float* p) { return V3{p[0], p[1], p[2]}; }
+// `c ? uv : V2{0, 0}` per component: the conditional on whole aggregates made
+// clang select between the addresses of two stack temporaries, which kept
+// them in scratch memory (k_shade spilled 44 B per lane)
+MRT_DEV V2 uv_or_zero(bool c, V2 uv) { return V2{c ? uv.x : 0.0f, c ? uv.y : 0.0f}; }
 
 // ---- textures -----------------------------------------------------------
 MRT_DEV float rust_fract(float x) { return x - truncf(x); }
@@ -500,9 +504,6 @@ MRT_DEV bool box_hit_any(V3 mn, V3 mx, const TRay& r, float tmin, float tmax, Lo
     slab_fast(mn, mx, r, tmin, tmax, t0, t1);
     const float m = slab_margin(r, t0, t1);
     const float gap = t1 - t0;
-#ifdef MRT_NO_FALLBACK  // experiment builds only (results NOT exact): cost of the exact fallback
-    return gap >= 0.0f;
-#endif
     if (gap > m) return true;
     if (-gap > m) return false;
   }
@@ -581,10 +582,6 @@ MRT_DEV void trav_box(const TravIn& in, Trav& t, LocalCounters& lc) {
 template <bool COUNT>
 MRT_DEV void trav_box_index(const TravIn& in, Trav& t, LocalCounters& lc) {
   if (COUNT) lc.node_visits++;
-#ifdef MRT_PAD_VALU  // experiment builds only: VALU sensitivity of the box run
-#pragma unroll
-  for (int k = 0; k < MRT_PAD_VALU; ++k) asm volatile("v_nop");
-#endif
   V3 mn{u2f(t.s0.x), u2f(t.s0.y), u2f(t.s0.z)}, mx{u2f(t.s0.w), u2f(t.s1.x), u2f(t.s1.y)};
   t.i = box_hit_any<COUNT>(mn, mx, t.r, in.tmin, t.best, &lc) ? (t.s1.w & ~kBoxFlag) : t.s1.z;
 }
@@ -639,13 +636,14 @@ MRT_DEV void trav_prim_index(const TravIn& in, Trav& t, LocalCounters& lc) {
     V3 a{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, ab{u2f(s0.w), u2f(s1.x), u2f(s1.y)}, ac{u2f(s2.x), u2f(s2.y), u2f(s2.z)};
     float th;
     if (tri_hit(a, ab, ac, t.r.o, t.r.d, in.tmin, t.best, th)) {
-      if (!ALPHA || !(s2.w & TRI_FLAG_ALPHA) || tri_alpha_pass<RNG, ALPHA == 2>(S, s1.z, t.r.o, t.r.d, th, t.rng, lc)) {
+      const uint32_t id = s1.z & kTriIdMask;
+      if (!ALPHA || !(s1.z & kTriAlpha) || tri_alpha_pass<RNG, ALPHA == 2>(S, id, t.r.o, t.r.d, th, t.rng, lc)) {
         t.best = th;
-        t.prim = make_ref(MRT_REF_TRIANGLE, s1.z);
+        t.prim = make_ref(MRT_REF_TRIANGLE, id);
         t.hit_ret = t.ret;
       }
     }
-    t.i += 3;
+    t.i = s2.w;
   } else if (kind == KIND_SPHERE) {
     if (COUNT) lc.sphere_tests++;
     float th;
@@ -654,7 +652,7 @@ MRT_DEV void trav_prim_index(const TravIn& in, Trav& t, LocalCounters& lc) {
       t.prim = make_ref(MRT_REF_SPHERE, s1.x);
       t.hit_ret = t.ret;
     }
-    t.i += 2;
+    t.i = s1.y;
   } else if (RNG && kind == KIND_VOLUME) {
     float th;
     if (volume_hit(S, in, t, s0, s1.x, th)) {
@@ -662,7 +660,7 @@ MRT_DEV void trav_prim_index(const TravIn& in, Trav& t, LocalCounters& lc) {
       t.prim = make_ref(MRT_REF_VOLUME, s1.x);
       t.hit_ret = t.ret;
     }
-    t.i += 2;
+    t.i = s1.y;
   } else if (kind == KIND_INST) {
     if (COUNT) lc.instance_entries++;
     V3 c0, c1, c2, c3;
@@ -745,7 +743,7 @@ MRT_DEV Surf resolve_hit(const DevScene& S, V3 o, V3 d, const Hit& h) {
     tri_bary(t, s.point, a0, a1, a2);
     outward = (t.na * a0 + t.nb * a1) + t.nc * a2;
     s.has_uv = (t.flags & TRI_FLAG_UV) != 0;
-    s.uv = s.has_uv ? (t.uva * a0 + t.uvb * a1) + t.uvc * a2 : V2{0, 0};
+    s.uv = uv_or_zero(s.has_uv, (t.uva * a0 + t.uvb * a1) + t.uvc * a2);
     s.material = t.material;
   }
   // Hit::set_face_normal in the intersecting (object) space (geom.rs:17-24)
@@ -875,7 +873,7 @@ MRT_DEV void lambertian(const DevScene& S, const GpuMaterial& m, const Surf& s, 
                         LocalCounters& lc) {
   V3 dir = s.normal + unit(random_in_unit_sphere(rng));
   if (near_zero(dir)) dir = s.normal;
-  V4 c = surface_get_f<EXT>(S, m, s.has_uv ? s.uv : V2{0, 0}, lc);
+  V4 c = surface_get_f<EXT>(S, m, uv_or_zero(s.has_uv, s.uv), lc);
   atten = V3{c.x, c.y, c.z};
   new_d = dir;
 }
@@ -890,7 +888,7 @@ MRT_DEV bool scatter(const DevScene& S, const Surf& s, V3 d, PathRng& rng, V3& e
     if (e.kind == MRT_MAT_DIFFUSE_LIGHT) emitted = V3{e.color[0], e.color[1], e.color[2]};
   }
   const GpuMaterial m = S.materials[mix_pick(S, s.material, rng)];
-  V2 uv = s.has_uv ? s.uv : V2{0, 0};
+  V2 uv = uv_or_zero(s.has_uv, s.uv);
   switch (m.kind) {
     case MRT_MAT_LAMBERTIAN:
       lambertian<EXT>(S, m, s, rng, atten, new_d, lc);

@@ -252,33 +252,6 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(ALPHA == 0 
       pool += n_idle < avail ? n_idle : avail;
       if (live == 0) break;  // chunk source exhausted
     }
-#ifdef MRT_UNIFIED_LOOP
-    // Experiment (MRT_UNIFIED_LOOP builds): every busy lane takes one step —
-    // a box test or a primitive/instance/region-end step — and then every
-    // lane that moved loads its next record with ONE pair of loads; repeat
-    // until enough lanes have finished to refill. Utilisation rises (0.60 ->
-    // 0.72) but each iteration runs both the box and the primitive code:
-    // 15-20% slower on sphere_grid / cube_field.
-    const uint32_t need = (pool == pool_end && drained) ? 64u * R : tune.refill * R;
-#pragma unroll
-    for (int q = 0; q < R; ++q) {
-      for (;;) {
-        const bool busy = !t[q].done;  // idle lanes hold a done Trav
-        if (busy) {
-          if (trav_at_box(t[q]))
-            trav_box_index<COUNT>(tin, t[q], lc);
-          else
-            trav_prim_index<COUNT, ALPHA, RNG, LDS>(tin, t[q], lc);
-        }
-        if (!t[q].done) trav_fetch<LDS>(tin, t[q]);
-        if (COUNT) {
-          lc.wave_slots += lane_id() == 0 ? 64u : 0u;
-          lc.lane_steps += busy ? 1u : 0u;
-        }
-        if ((uint32_t)__popcll(__builtin_amdgcn_ballot_w64(t[q].done)) >= need) break;
-      }
-    }
-#else
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       // box run: keep stepping boxes with little per-step overhead while at
@@ -291,20 +264,10 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(ALPHA == 0 
         if ((uint32_t)__popcll(bm) < tune.box_min) break;
         if (run_box) trav_box_index<COUNT>(tin, t[q], lc);
         if (run_box) trav_fetch<LDS>(tin, t[q]);
-#ifdef MRT_PROBE  // experiment builds: texel_taps = box-run iterations, wave_slots = uniform ones
-        if (COUNT) {
-          const uint32_t f = __builtin_amdgcn_readfirstlane(run_box ? t[q].i : 0xFFFFFFFFu);
-          const bool uni = __builtin_amdgcn_ballot_w64(run_box && t[q].i != f) == 0;
-          lc.texel_taps += lane_id() == 0 ? 1u : 0u;
-          lc.wave_slots += (lane_id() == 0 && uni) ? 1u : 0u;
-          lc.lane_steps += run_box ? 1u : 0u;
-        }
-#else
         if (COUNT) {
           lc.wave_slots += lane_id() == 0 ? 64u : 0u;
           lc.lane_steps += run_box ? 1u : 0u;
         }
-#endif
       }
       const bool busy = !t[q].done;  // idle lanes hold a done Trav
       const bool at_box = busy && trav_at_box(t[q]);
@@ -314,17 +277,11 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(ALPHA == 0 
       // primitives wait until enough lanes are at one (or no lane is at a box)
       const bool prim_go = (__popcll(prim_mask) >= tune.prim_batch || box_mask == 0) && busy && !at_box;
       if (prim_go) trav_prim<COUNT, ALPHA, RNG, LDS>(tin, t[q], lc);
-#ifdef MRT_PROBE
-      if (COUNT) lc.model_entries += lane_id() == 0 ? 1u : 0u;  // outer iterations
-#endif
       if (COUNT) {
-#ifndef MRT_PROBE
         lc.wave_slots += lane_id() == 0 ? 64u : 0u;
-#endif
         lc.lane_steps += (at_box || prim_go) ? 1u : 0u;
       }
     }
-#endif
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       if (t[q].ray != kIdle && t[q].done) {

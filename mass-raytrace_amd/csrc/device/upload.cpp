@@ -2,6 +2,7 @@
 #include "upload.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -156,18 +157,20 @@ struct Emitter {
   // primitive of the region lands on it, so the device never compares the
   // record index against the region's end.
   void push_end() {
+    s.rec_starts.push_back(n_slots());
     push_slot(0, 0, 0, 0);
     push_slot(0, 0, 0, KIND_END);
   }
 
   bool emit_prim(uint32_t ref, bool in_blas) {
     uint32_t kind = MRT_REF_KIND(ref), idx = MRT_REF_INDEX(ref);
+    s.rec_starts.push_back(n_slots());  // (a failed emission aborts the whole build)
     switch (kind) {
       case MRT_REF_SPHERE: {
         if (idx >= d.n_spheres) return fail("sphere index out of range");
         const mrt_sphere& sp = d.spheres[idx];
-        push_slot(fbits(sp.center[0]), fbits(sp.center[1]), fbits(sp.center[2]), fbits(sp.radius));
-        push_slot(idx, 0, 0, KIND_SPHERE);
+        const uint32_t at = push_slot(fbits(sp.center[0]), fbits(sp.center[1]), fbits(sp.center[2]), fbits(sp.radius));
+        push_slot(idx, at + 2, 0, KIND_SPHERE);  // next: the following record
         s.n_prim_records++;
         return true;
       }
@@ -176,15 +179,15 @@ struct Emitter {
         const mrt_triangle& t = d.triangles[idx];
         float ab[3], ac[3];
         for (int k = 0; k < 3; ++k) ab[k] = t.b[k] - t.a[k], ac[k] = t.c[k] - t.a[k];
-        uint32_t flags = 0;
-        if (t.flags & MRT_TRI_HAS_UV) flags |= TRI_FLAG_UV;
+        if (idx > kTriIdMask) return fail("triangle index too large");
+        uint32_t id = idx;
         if (needs_alpha(t)) {
-          flags |= TRI_FLAG_ALPHA;
+          id |= kTriAlpha;
           s.has_alpha = true;
         }
-        push_slot(fbits(t.a[0]), fbits(t.a[1]), fbits(t.a[2]), fbits(ab[0]));
-        push_slot(fbits(ab[1]), fbits(ab[2]), idx, KIND_TRI);
-        push_slot(fbits(ac[0]), fbits(ac[1]), fbits(ac[2]), flags);
+        const uint32_t at = push_slot(fbits(t.a[0]), fbits(t.a[1]), fbits(t.a[2]), fbits(ab[0]));
+        push_slot(fbits(ab[1]), fbits(ab[2]), id, KIND_TRI);
+        push_slot(fbits(ac[0]), fbits(ac[1]), fbits(ac[2]), at + 3);  // next: the following record
         s.n_prim_records++;
         return true;
       }
@@ -192,8 +195,8 @@ struct Emitter {
         if (idx >= d.n_volumes) return fail("volume index out of range");
         if (in_blas) return fail("a Volume must be a World object (not inside a model)");
         const mrt_volume& v = d.volumes[idx];
-        push_slot(fbits(v.center[0]), fbits(v.center[1]), fbits(v.center[2]), fbits(v.radius));
-        push_slot(idx, 0, 0, KIND_VOLUME);
+        const uint32_t at = push_slot(fbits(v.center[0]), fbits(v.center[1]), fbits(v.center[2]), fbits(v.radius));
+        push_slot(idx, at + 2, 0, KIND_VOLUME);
         s.n_prim_records++;
         s.trav_rng = true;
         return true;
@@ -273,6 +276,7 @@ struct Emitter {
           if (!(a <= 0x1p28f)) s.early_ok = 0;  // NaN and inf too
         }
       }
+      s.rec_starts.push_back(n_slots());
       uint32_t at = push_slot(fbits(n.min[0]), fbits(n.min[1]), fbits(n.min[2]), fbits(n.max[0]));
       push_slot(fbits(n.max[1]), fbits(n.max[2]), 0, kBoxFlag | (at + 2));  // hit: the first child, next
       s.n_box_records++;
@@ -285,6 +289,115 @@ struct Emitter {
     return true;
   }
 };
+
+// ---- record helpers (layout.h) ----
+uint32_t rec_kind(const std::vector<uint32_t>& w, uint32_t i) { return w[4 * (i + 1) + 3]; }
+bool rec_is_box(const std::vector<uint32_t>& w, uint32_t i) { return (rec_kind(w, i) & kBoxFlag) != 0; }
+uint32_t rec_slots(const std::vector<uint32_t>& w, uint32_t i) {
+  const uint32_t k = rec_kind(w, i);
+  return (k & kBoxFlag) ? 2 : (k == KIND_TRI ? 3 : 2);
+}
+// the record the traversal reaches after primitive / instance record i
+uint32_t rec_next(const std::vector<uint32_t>& w, uint32_t i) {
+  switch (rec_kind(w, i)) {
+    case KIND_TRI: return w[4 * (i + 2) + 3];
+    case KIND_SPHERE:
+    case KIND_VOLUME: return w[4 * (i + 1) + 1];
+    default: return i + 2;  // instance / model: the record after it
+  }
+}
+// children of box record i, in order (the first is its hit index; a child's
+// successor at its level: a box's skip, a primitive's next)
+void box_children(const std::vector<uint32_t>& w, uint32_t i, std::vector<uint32_t>& out) {
+  out.clear();
+  const uint32_t end = w[4 * (i + 1) + 2];
+  for (uint32_t c = rec_kind(w, i) & ~kBoxFlag; c != end; c = rec_is_box(w, c) ? w[4 * (c + 1) + 2] : rec_next(w, c))
+    out.push_back(c);
+}
+
+// BLAS regions laid out with siblings together (round 3): the
+// region's root first, then every box's children as one group, the groups in
+// depth-first order of their parents, each group starting on a 64-byte
+// boundary, the END record last. The traversal's sequence of records is
+// unchanged (every successor is explicit); what changes is which records
+// share a cache line: a box and its sibling sit in one 64-B half-line, so a
+// ray that tests both fetches one line, where the preorder stream put the
+// sibling after the whole left subtree. tools/layout_sim.cpp, mesh_ply: 64 ->
+// 40 distinct 128-B lines per ray, L2 misses 1.67 -> 1.29 per ray (model).
+// The world region keeps its preorder layout: instance and model records
+// return to the record after them.
+void relayout_blas(HostScene& s) {
+  if (s.blas_regions.empty()) return;
+  const std::vector<uint32_t>& w = s.slots;
+  uint32_t first = s.blas_regions[0].begin;
+  for (const BlasRegion& r : s.blas_regions) first = std::min(first, r.begin);
+  std::vector<uint32_t> out(w.begin(), w.begin() + 4 * (size_t)first);  // the world region as it is
+  std::vector<uint32_t> remap(w.size() / 4, ~0u);
+  std::vector<uint32_t> kids, order, stack;
+  for (BlasRegion& r : s.blas_regions) {
+    // order: root, then each box's children group (parents in DFS order)
+    order.assign(1, r.begin);
+    std::vector<uint8_t> group_start;  // parallel to order
+    group_start.assign(1, 1);
+    stack.assign(1, r.begin);
+    while (!stack.empty()) {
+      const uint32_t b = stack.back();
+      stack.pop_back();
+      if (!rec_is_box(w, b)) continue;
+      box_children(w, b, kids);
+      for (size_t k = 0; k < kids.size(); ++k) {
+        order.push_back(kids[k]);
+        group_start.push_back(k == 0);
+      }
+      for (size_t k = kids.size(); k-- > 0;)
+        if (rec_is_box(w, kids[k])) stack.push_back(kids[k]);
+    }
+    order.push_back(r.end);  // END
+    group_start.push_back(1);
+    // positions: 8-slot (128-B) aligned region start, 4-slot (64-B) aligned groups
+    uint32_t at = (uint32_t)(out.size() / 4);
+    at = (at + 7) & ~7u;
+    for (size_t k = 0; k < order.size(); ++k) {
+      if (group_start[k]) at = (at + 3) & ~3u;
+      remap[order[k]] = at;
+      at += rec_slots(w, order[k]);
+    }
+    out.resize(4 * (size_t)at, 0u);
+    for (uint32_t o : order) {
+      const uint32_t n = remap[o];
+      const uint32_t sl = rec_slots(w, o);
+      std::copy(w.begin() + 4 * (size_t)o, w.begin() + 4 * (size_t)(o + sl), out.begin() + 4 * (size_t)n);
+      uint32_t* rec = &out[4 * (size_t)n];
+      const uint32_t k = rec_kind(w, o);
+      if (k & kBoxFlag) {
+        rec[6] = remap[rec[6]];
+        rec[7] = kBoxFlag | remap[rec[7] & ~kBoxFlag];
+      } else if (k == KIND_TRI) {
+        rec[11] = remap[rec[11]];
+      } else if (k == KIND_SPHERE || k == KIND_VOLUME) {
+        rec[5] = remap[rec[5]];
+      }
+    }
+    const uint32_t nb = remap[r.begin], ne = remap[r.end];
+    r.begin = nb;
+    r.end = ne;
+  }
+  // instance / model records of the world: their BLAS ranges
+  for (uint32_t i : s.rec_starts) {
+    if (i >= first) break;
+    const uint32_t k = rec_kind(w, i);
+    if (k == KIND_INST || k == KIND_MODEL) {
+      out[4 * (size_t)i + 1] = remap[w[4 * (size_t)i + 1]];
+      out[4 * (size_t)i + 2] = remap[w[4 * (size_t)i + 2]];
+    }
+  }
+  std::vector<uint32_t> starts;
+  for (uint32_t i : s.rec_starts)
+    starts.push_back(i < first ? i : remap[i]);
+  std::sort(starts.begin(), starts.end());
+  s.rec_starts.swap(starts);
+  s.slots.swap(out);
+}
 
 void put_m4_12(std::vector<float>& dst, const float* m16) {
   // column-major 4x4 -> c0.xyz c1.xyz c2.xyz c3.xyz
@@ -422,6 +535,8 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
     s.slots[4 * p.first + 2] = r.end;
   }
   if (e.mix_alpha) s.trav_rng = true;
+  const char* lay = getenv("MRT_LAYOUT");  // "dfs": keep the preorder stream (A/B)
+  if (!(lay && !strcmp(lay, "dfs"))) relayout_blas(s);
   if (s.slots.size() / 4 >= kLdsTag) return (err = "scene too large (record stream >= 2^30 slots)", false);
   return true;
 }
@@ -430,11 +545,6 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
 
 namespace {
 
-uint32_t rec_slots(const std::vector<uint32_t>& w, uint32_t i) {
-  const uint32_t k = w[4 * (i + 1) + 3];
-  return (k & kBoxFlag) ? 2 : (k == KIND_TRI ? 3 : 2);
-}
-bool rec_is_box(const std::vector<uint32_t>& w, uint32_t i) { return (w[4 * (i + 1) + 3] & kBoxFlag) != 0; }
 double box_area(const std::vector<uint32_t>& w, uint32_t i) {
   float v[6];
   memcpy(v, &w[4 * i], 16);
@@ -457,8 +567,11 @@ void build_treelet(HostScene& s, uint32_t budget) {
   std::vector<uint8_t> staged(n, 0);  // record starts chosen for the LDS copy
   uint32_t used = 0;
   auto stage_range = [&](uint32_t b, uint32_t e) {  // every record of [b, e)
-    for (uint32_t i = b; i < e; i += rec_slots(w, i)) staged[i] = 1;
-    used += e - b;
+    for (auto it = std::lower_bound(s.rec_starts.begin(), s.rec_starts.end(), b);
+         it != s.rec_starts.end() && *it < e; ++it) {
+      staged[*it] = 1;
+      used += rec_slots(w, *it);
+    }
   };
   if (n <= budget) {
     stage_range(0, n);  // small scene: the whole stream
@@ -484,13 +597,14 @@ void build_treelet(HostScene& s, uint32_t budget) {
     //    the world roots and the roots of model BLAS (same space): a child's
     //    area never exceeds its parent's, so the chosen set is a rooted treelet
     std::priority_queue<std::pair<double, uint32_t>> pq;
+    std::vector<uint32_t> kids;
     auto push_children = [&](uint32_t i) {
-      for (uint32_t j = i + 2, end = w[4 * (i + 1) + 2]; j < end;
-           j = rec_is_box(w, j) ? w[4 * (j + 1) + 2] : j + rec_slots(w, j))
+      box_children(w, i, kids);
+      for (uint32_t j : kids)
         if (rec_is_box(w, j) && !staged[j]) pq.push({box_area(w, j), j});
     };
     for (uint32_t j = s.world_begin; j < n && w[4 * (j + 1) + 3] != KIND_END;
-         j = rec_is_box(w, j) ? w[4 * (j + 1) + 2] : j + rec_slots(w, j))
+         j = rec_is_box(w, j) ? w[4 * (j + 1) + 2] : rec_next(w, j))
       if (rec_is_box(w, j)) pq.push({box_area(w, j), j});
     for (size_t k = 0; k < s.blas_regions.size(); ++k)
       if (!whole[k] && s.blas_regions[k].model && rec_is_box(w, s.blas_regions[k].begin))
@@ -503,28 +617,34 @@ void build_treelet(HostScene& s, uint32_t budget) {
       push_children(i);
     }
   }
-  // LDS image: the chosen records in stream order (whole regions stay contiguous)
+  // LDS image: the chosen records in stream order (whole regions stay together)
   std::vector<uint32_t> lds_at(n, ~0u);
-  for (uint32_t i = 0, at = 0; i < n; i += rec_slots(w, i))
+  uint32_t at = 0;
+  for (uint32_t i : s.rec_starts)
     if (staged[i]) {
       lds_at[i] = at;
       at += rec_slots(w, i);
       if (rec_is_box(w, i)) s.tl_boxes++;
-      const uint32_t nx = i + rec_slots(w, i);
-      if (!rec_is_box(w, i) && w[4 * (i + 1) + 3] != KIND_END && !(nx < n && staged[nx]))
-        throw std::logic_error("treelet: a copied primitive's next record is not copied");
     }
+  for (uint32_t i : s.rec_starts)  // an instance/model returns to the record after it: that one too
+    if (staged[i] && (rec_kind(w, i) == KIND_INST || rec_kind(w, i) == KIND_MODEL) &&
+        !(i + 2 < n && staged[i + 2] && lds_at[i + 2] == lds_at[i] + 2))
+      throw std::logic_error("treelet: a copied instance's successor is not copied after it");
   auto R = [&](uint32_t g) { return g < n && lds_at[g] != ~0u ? (kLdsTag | lds_at[g]) : g; };
-  auto rewrite = [&](uint32_t* rec) {  // rec: 8 words of one record's first two slots
+  auto rewrite = [&](uint32_t* rec) {  // rec: one record's slots (4 words each)
     if (rec[7] & kBoxFlag) {
       rec[6] = R(rec[6]);
       rec[7] = kBoxFlag | R(rec[7] & ~kBoxFlag);
     } else if (rec[7] == KIND_INST || rec[7] == KIND_MODEL) {
       rec[1] = R(rec[1]);
+    } else if (rec[7] == KIND_TRI) {
+      rec[11] = R(rec[11]);
+    } else if (rec[7] == KIND_SPHERE || rec[7] == KIND_VOLUME) {
+      rec[5] = R(rec[5]);
     }
   };
   s.slots_tl = w;
-  for (uint32_t i = 0; i < n; i += rec_slots(w, i)) {
+  for (uint32_t i : s.rec_starts) {
     rewrite(&s.slots_tl[4 * i]);
     if (staged[i]) {
       const size_t at = s.tlet.size();

@@ -16,6 +16,7 @@ struct BlasRegion {
 
 struct HostScene {
   std::vector<uint32_t> slots;  // 4 words per slot
+  std::vector<uint32_t> rec_starts;  // first slot of every record, ascending (padding slots are not records)
   uint32_t world_begin = 0, world_end = 0;
   std::vector<float> inst_inv, inst_fwd;
   std::vector<uint32_t> inst_mat, model_mat;

@@ -1,0 +1,69 @@
+#!/bin/bash
+# One parameterised GPU-box session (replaces round 1-2's one-off gpu_*.sh).
+# Every GPU step has its own time limit; steps chain with && so the first
+# failure (fault, abort, time limit) ends the session — no step is retried.
+#
+#   bash tools/gpu_session.sh tests                 # pytest -m gpu + smoke
+#   bash tools/gpu_session.sh bench [bench args]    # the default bench line (+ args)
+#   bash tools/gpu_session.sh profile SCENE...      # rocprofv3 stats + stamped PMC (tools/profile.sh)
+#   bash tools/gpu_session.sh configs               # every BASELINE config scene, timing only
+#   LABELS="a b" LIBS="x.so y.so" bash tools/gpu_session.sh ab   # bench per library build (MASSRT_LIB)
+#   SWEEP=$'base\ntl MRT_TREELET_KB=16' bash tools/gpu_session.sh sweep   # bench per env configuration
+# SCENES (default "sphere_grid mesh_ply") and STEPS (default 6) apply to ab / sweep.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/session
+MODE=$1; shift
+SCENES=${SCENES:-"sphere_grid mesh_ply"}
+STEPS=${STEPS:-6}
+
+line() {  # log, label: one summary line of a bench log
+  python3 -c "import json,sys; j=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=j['roofline'] or {}; s=j.get('roofline_k_shade') or {}
+print('%-28s %-12s %8.1f Msamples/s  %8.1f ms/step  k_trace %.3f ms  k_shade %.3f ms  util %.3f' % (sys.argv[2], j['config']['scene'], j['value'], j['ms_per_step'], r.get('avg_launch_ms', 0), s.get('avg_launch_ms', 0), r.get('lane_utilisation', 0)))" "$1" "$2"
+}
+quick() {  # label, log, bench args...: a timing-only bench of one scene
+  local label=$1 log=$2; shift 2
+  timeout -k 10 400 python bench.py --secondary none --no-cpu-baseline --no-dropin "$@" > $log 2>&1 || { echo "FAILED $label"; tail -5 $log; return 1; }
+  line $log $label
+}
+
+case $MODE in
+  tests)
+    timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      > gpurun_out/session/pytest_gpu.log 2>&1 && tail -1 gpurun_out/session/pytest_gpu.log &&
+    timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/session/smoke.log 2>&1 &&
+    tail -1 gpurun_out/session/smoke.log ;;
+  bench)
+    timeout -k 10 900 python -u bench.py "$@" > gpurun_out/session/bench.log 2> gpurun_out/session/bench.err &&
+    line gpurun_out/session/bench.log headline ;;
+  profile)
+    for sc in "$@"; do SCENE=$sc bash tools/profile.sh > gpurun_out/session/profile_$sc.log 2>&1 || exit 1; done ;;
+  configs)
+    quick c2_sphere_grid gpurun_out/session/c2.log --scene sphere_grid --steps 8 &&
+    quick c3_cube_field gpurun_out/session/c3.log --scene cube_field --steps 6 &&
+    quick c4_mesh_ply gpurun_out/session/c4p.log --scene mesh_ply --steps 8 &&
+    quick c4_mesh_obj gpurun_out/session/c4o.log --scene mesh_obj --steps 8 &&
+    quick c5_mesh_obj_textured_4k gpurun_out/session/c5.log --scene mesh_obj_textured --width 3840 --height 2160 \
+      --spp-per-step 16 --total-spp 4096 --steps 6 &&
+    quick menger gpurun_out/session/menger.log --scene menger --steps 2 ;;
+  ab)
+    set -- $LIBS; labels=($LABELS); k=0
+    for lib in "$@"; do
+      lab=${labels[$k]:-$(basename $lib .so)}; k=$((k + 1))
+      for sc in $SCENES; do
+        MASSRT_LIB=$lib quick "$lab" gpurun_out/session/ab_${lab}_$sc.log --scene $sc --steps $STEPS || exit 1
+      done
+    done ;;
+  sweep)
+    while IFS= read -r cfg; do
+      [ -z "$cfg" ] && continue
+      set -- $cfg; lab=$1; shift
+      for sc in $SCENES; do
+        log=gpurun_out/session/sweep_${lab}_$sc.log
+        env "$@" timeout -k 10 400 python bench.py --scene $sc --secondary none --no-cpu-baseline --no-dropin \
+          --steps $STEPS > $log 2>&1 || { echo "FAILED $lab $sc"; tail -5 $log; exit 1; }
+        line $log $lab
+      done
+    done <<< "$SWEEP" ;;
+  *) echo "unknown mode $MODE"; exit 2 ;;
+esac

@@ -153,13 +153,13 @@ Result walk_plain(const HostScene& s, V o, V d, Stats* st = nullptr) {
       float t;
       if (sphere_hit({f(a[0]), f(a[1]), f(a[2])}, f(a[3]), r.o, r.d, kTmin, best, t))
         best = t, prim = MRT_REF(MRT_REF_SPHERE, a[4]), hit_ret = ret;
-      i += 2;
+      i = a[5];  // next (layout.h)
     } else if (k == KIND_TRI) {
       float t;
       if (tri_hit({f(a[0]), f(a[1]), f(a[2])}, {f(a[3]), f(a[4]), f(a[5])}, {f(a[8]), f(a[9]), f(a[10])}, r.o, r.d,
                   kTmin, best, t))
-        best = t, prim = MRT_REF(MRT_REF_TRIANGLE, a[6]), hit_ret = ret;
-      i += 3;
+        best = t, prim = MRT_REF(MRT_REF_TRIANGLE, a[6] & kTriIdMask), hit_ret = ret;
+      i = a[11];  // next (layout.h)
     } else if (k == KIND_INST) {
       const float* m = &s.inst_inv[12 * (size_t)a[0]];
       r = make_ray(xf(m, wr.o, 1.0f), xf(m, wr.d, 0.0f), s.early_ok);
@@ -202,6 +202,17 @@ int main(int argc, char** argv) {
     printf("%s\n", err.c_str());
     return 1;
   }
+  // `layout` mode: the same rays through the preorder stream (MRT_LAYOUT=dfs)
+  // and the default layout (BLAS regions with siblings together) must find the
+  // same closest hits, t bits included, after the same number of box tests
+  HostScene dfs;
+  const bool layout = argc > 4 && !strcmp(argv[4], "layout");
+  if (layout) {
+    setenv("MRT_LAYOUT", "dfs", 1);
+    if (!build_host_scene(d, dfs, err)) return 1;
+    unsetenv("MRT_LAYOUT");
+  }
+  uint64_t layout_bad = 0;
   std::mt19937 g(7);
   std::uniform_real_distribution<float> u(0.0f, 1.0f);
   Stats st;
@@ -224,7 +235,22 @@ int main(int argc, char** argv) {
       rd = {u(g) * 2 - 1, u(g) * 2 - 1, u(g) * 2 - 1};
     }
     fast += make_ray(ro, rd, s.early_ok).fast;
-    hits += walk_plain(s, ro, rd, &st).prim != 0;
+    const uint64_t boxes0 = st.boxes;
+    const Result r = walk_plain(s, ro, rd, &st);
+    hits += r.prim != 0;
+    if (layout) {
+      Stats sd;
+      const Result q = walk_plain(dfs, ro, rd, &sd);
+      uint32_t tb, qb;
+      memcpy(&tb, &r.t, 4);
+      memcpy(&qb, &q.t, 4);
+      layout_bad += r.prim != q.prim || r.container != q.container || tb != qb || sd.boxes != st.boxes - boxes0;
+    }
+  }
+  if (layout) {
+    printf("%-14s layout: %llu of %d rays differ between the sibling layout and the preorder stream; stream %zu vs %zu slots\n",
+           argv[1], (unsigned long long)layout_bad, n, s.slots.size() / 4, dfs.slots.size() / 4);
+    if (layout_bad) return 1;
   }
   printf("%-14s rays %d (early domain %llu) hits %llu  boxes %llu  left to the exact test %.5f  wrong %llu\n", argv[1],
          n, (unsigned long long)fast, (unsigned long long)hits, (unsigned long long)st.boxes,
