@@ -1,0 +1,38 @@
+"""The record-stream layout (layout.h, upload.cpp relayout_blas) on the host,
+no GPU: the same rays through the preorder stream (MRT_LAYOUT=dfs) and
+through the default layout (BLAS regions with siblings together, every
+successor explicit) find the same closest hits, t bits included, after the
+same number of box tests; the early slab decision stays exact
+(tools/slab_check.cpp, which restates k_trace's walk on the host)."""
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import GOLDEN, REPO
+
+
+@pytest.fixture(scope="module")
+def slab_check(tmp_path_factory):
+    if not shutil.which("g++"):
+        pytest.skip("g++ missing")
+    exe = tmp_path_factory.mktemp("slab") / "slab_check"
+    lib = REPO / "mass-raytrace_amd" / "massrt"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe), str(REPO / "tools" / "slab_check.cpp"),
+                    f"-L{lib}", "-lmassrt", f"-Wl,-rpath,{lib}"], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("scene", ["cornell", "sphere_grid", "cube_field"])
+def test_sibling_layout_walks_like_the_preorder_stream(slab_check, scene):
+    r = subprocess.run([str(slab_check), scene, "20000", str(GOLDEN), "layout"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 of 20000 rays differ" in r.stdout, r.stdout
+
+
+@pytest.mark.slow
+def test_sibling_layout_mesh(slab_check, assets_dir):
+    r = subprocess.run([str(slab_check), "mesh_ply", "20000", str(assets_dir), "layout"], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0 and " 0 of 20000 rays differ" in r.stdout, r.stdout + r.stderr

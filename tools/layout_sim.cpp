@@ -46,7 +46,10 @@ struct Stream {
   uint32_t size(uint32_t i) const { return box(i) ? 2 : (kind(i) == KIND_TRI ? 3 : 2); }
   uint32_t hit(uint32_t i) const { return kind(i) & ~kBoxFlag; }
   uint32_t skip(uint32_t i) const { return w[4 * (i + 1) + 2]; }
-  uint32_t next(uint32_t i) const { return kind(i) == KIND_TRI ? w[4 * (i + 2) + 3] : w[4 * (i + 1) + 1]; }
+  uint32_t next(uint32_t i) const {
+    const uint32_t k = kind(i);
+    return k == KIND_TRI ? w[4 * (i + 2) + 3] : (k == KIND_INST || k == KIND_MODEL) ? i + 2 : w[4 * (i + 1) + 1];
+  }
 };
 
 struct Ray {
@@ -144,7 +147,6 @@ static Tree parse(const Stream& s, uint32_t begin) {
       t.kids[i] = k;
     }
     i += s.size(i);
-    while (i < s.w.size() / 4 && s.w[4 * i + 4 + 3] == 0 && s.w[4 * i] == 0 && s.w[4 * i + 1] == 0 && false) ++i;
   }
   t.recs.push_back(i);  // END
   return t;
@@ -167,13 +169,14 @@ static Layout pack(const Stream& s, const std::vector<uint32_t>& order, uint32_t
 // packed in order, every sibling group (a node's children) starting on a
 // `galign`-byte boundary, triangles padded to `tri` bytes
 static Layout pack_groups(const Stream& s, const Tree& t, const std::vector<uint32_t>& order, uint32_t galign,
-                          uint32_t tri) {
+                          uint32_t tri, uint32_t prim_galign = 0) {
   std::unordered_map<uint32_t, bool> first;  // first record of a sibling group
   for (auto& kv : t.kids) first[kv.second.front()] = true;
   Layout L;
   uint64_t a = 0;
   for (uint32_t r : order) {
-    if (first.count(r)) a = (a + galign - 1) / galign * galign;
+    const uint32_t ga = (prim_galign && !s.box(r)) ? prim_galign : galign;
+    if (first.count(r)) a = (a + ga - 1) / ga * ga;
     L[r] = a;
     a += (s.kind(r) == KIND_TRI) ? tri : 16 * s.size(r);
   }
@@ -262,6 +265,7 @@ int main(int argc, char** argv) {
   const char* scene = argc > 1 ? argv[1] : "mesh_ply";
   const char* assets = argc > 2 ? argv[2] : "assets";
   const int nrays = argc > 3 ? atoi(argv[3]) : 200000;
+  setenv("MRT_LAYOUT", "dfs", 1);  // the preorder stream: the layouts below are made from it
   mrt_builder* b = nullptr;
   mrt_builder_new(1, &b);
   if (mrt_builder_builtin(b, scene, 16.0f / 9.0f, assets) != MRT_OK) {
@@ -342,6 +346,8 @@ int main(int argc, char** argv) {
   cands.push_back({"sibling pairs, 32-B", pack(s, sibling_order(s, t, begin), 32)});
   cands.push_back({"sibling pairs, groups 64-B", pack_groups(s, t, sibling_order(s, t, begin), 64, 48)});
   cands.push_back({"sibling pairs, grp 64, tri 64", pack_groups(s, t, sibling_order(s, t, begin), 64, 64)});
+  cands.push_back({"sib, box grp 64, prim grp 16", pack_groups(s, t, sibling_order(s, t, begin), 64, 48, 16)});
+  cands.push_back({"sib, box grp 64, prim grp 32", pack_groups(s, t, sibling_order(s, t, begin), 64, 48, 32)});
   cands.push_back({"sibling pairs, grp 128, tri 64", pack_groups(s, t, sibling_order(s, t, begin), 128, 64)});
   for (size_t hot : {1024, 16384, 131072}) cands.push_back({"hot " + std::to_string(hot) + " first", pack(s, hot_first(s, t, begin, hot), 16)});
   for (int dep : {2, 3, 4}) cands.push_back({"clusters depth " + std::to_string(dep), pack(s, clustered(s, t, begin, dep), 16)});
