@@ -36,10 +36,18 @@ roofline (dominant kernel k_trace, closest hit):
              hash) matches this run; else null.
   bound    = the unit the PMC counters show busiest (TA/L1 address path, HBM,
              VALU), e.g. "l1/ta" for SphereGrid.
+roofline_k_shade: k_shade (path-state streaming) against HBM, 176 B per
+  shaded path, with the PMC traffic/limiter of the same stamped profile.
 cpu_baseline: the oracle's reference-mode restatement (main.rs:159-290
 threading: num_cpus-2 workers rendering whole 1-spp passes) on a stratified
 sample of rows spread over the whole frame, rank 0 at N=1 only, plus an
-all-logical-cores run; host model and core counts are recorded.
+all-logical-cores run; host model and core counts are recorded;
+gpu_over_cpu is against the whole host (host_estimate when the job has a
+CPU quota), gpu_over_cpu_quota<N> against the job's share.
+config.dropin: the Rust binding's render() call pattern (massrt.render:
+pre-pass, clear, num_cpus-2 passes per frame in batches of 64 into the
+device-resident image, a tonemap + host copy per batch), 1080p, both scenes.
+--gpus N without a launcher starts N ranks itself (torch.distributed.run).
 """
 from __future__ import annotations
 
