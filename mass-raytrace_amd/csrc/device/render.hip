@@ -404,8 +404,10 @@ __global__ __launch_bounds__(kBlock, MRT_SHADE_WPE) void k_shade(DevScene S, Dev
     // regenerate finished slots from the work counter and compact survivors
     // into the next pool: one atomic per workgroup for each (same-address
     // atomics from every wave serialise in L2)
+    // (work == nullptr: the host saw the work counter exhausted — no
+    // reservation, and no barrier round or device atomic for it)
     const unsigned long long need_mask = __ballot(need);
-    const uint32_t wbase = wg_reserve(work, (uint32_t)__popcll(need_mask), wave, s_cnt, s_base);
+    const uint32_t wbase = work ? wg_reserve(work, (uint32_t)__popcll(need_mask), wave, s_cnt, s_base) : rp.G;
     if (need) {
       uint32_t g = wbase + lane_rank(need_mask);
       if (g < rp.G) {
@@ -1411,6 +1413,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
       int slot = 0;
       bool pending = false, finished = false;
       size_t bound = ~(size_t)0;  // live paths at most (shade_grid)
+      bool exhausted = false;     // the work counter was seen at or past G: k_shade need not regenerate
     } st_[kMaxQueues];
     int open = K;
     while (open > 0) {
@@ -1443,7 +1446,8 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
             auto* shade = count ? (c->scene_ext ? k_shade<true, true> : k_shade<true, false>)
                                 : (c->scene_ext ? k_shade<false, true> : k_shade<false, false>);
             hipLaunchKernelGGL(shade, dim3(shade_grid(q, L.bound)), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, q.bufs[cur],
-                               q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, work, res, c->d_cnt);
+                               q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, L.exhausted ? nullptr : work, res,
+                               c->d_cnt);
           }
           HIP_CHECK(hipGetLastError());
           if (timing) {
@@ -1461,7 +1465,10 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
           if (s.shade_short)
             throw ApiError{MRT_ERR_HIP, "internal: a k_shade grid was smaller than its live pool (" +
                                             std::to_string(s.shade_short) + " paths)"};
-          if (q.h_work[L.slot ^ 1] >= rp.G) L.bound = std::min<size_t>(L.bound, s.active[0]);
+          if (q.h_work[L.slot ^ 1] >= rp.G) {
+            L.bound = std::min<size_t>(L.bound, s.active[0]);
+            L.exhausted = true;
+          }
           if (q.h_work[L.slot ^ 1] >= rp.G && s.active[0] <= finish_paths) {
             // no new work: the paths left (at most as many as that status
             // showed) finish in one fused launch after the batch just queued

@@ -315,61 +315,72 @@ void box_children(const std::vector<uint32_t>& w, uint32_t i, std::vector<uint32
     out.push_back(c);
 }
 
-// BLAS regions laid out with siblings together (round 3): the
-// region's root first, then every box's children as one group, the groups in
-// depth-first order of their parents, each group starting on a 64-byte
-// boundary (32 B for a group of primitives), the END record last. The traversal's sequence of records is
-// unchanged (every successor is explicit); what changes is which records
-// share a cache line: a box and its sibling sit in one 64-B half-line, so a
-// ray that tests both fetches one line, where the preorder stream put the
-// sibling after the whole left subtree. tools/layout_sim.cpp, mesh_ply: 64 ->
-// 39 distinct 128-B lines per ray, L2 misses 1.67 -> 1.21 per ray (model;
-// measured on the GPU: mesh_ply k_trace 9.40 -> 8.95 ms, 681 -> 716 Msamples/s).
-// The world region keeps its preorder layout: instance and model records
-// return to the record after them.
-void relayout_blas(HostScene& s) {
-  if (s.blas_regions.empty()) return;
-  const std::vector<uint32_t>& w = s.slots;
-  uint32_t first = s.blas_regions[0].begin;
-  for (const BlasRegion& r : s.blas_regions) first = std::min(first, r.begin);
-  std::vector<uint32_t> out(w.begin(), w.begin() + 4 * (size_t)first);  // the world region as it is
-  std::vector<uint32_t> remap(w.size() / 4, ~0u);
-  std::vector<uint32_t> kids, order, stack;
-  for (BlasRegion& r : s.blas_regions) {
-    // order: root, then each box's children group (parents in DFS order)
-    order.assign(1, r.begin);
-    std::vector<uint8_t> group_start;  // parallel to order
-    group_start.assign(1, 8);
-    stack.assign(1, r.begin);
+// Regions laid out with siblings together (round 3): the
+// region's top-level items first, then every box's children as one group,
+// the groups in depth-first order of their parents; a group holding a box
+// starts on a 64-byte boundary, a group of primitives on 32 B; the END
+// record last. The traversal's sequence of records is unchanged (successors
+// are explicit); what changes is which records share a cache line: a box
+// and its sibling sit in one 64-B half-line, so a ray that tests both
+// fetches one line, where the preorder stream put the sibling after the whole
+// left subtree. tools/layout_sim.cpp, mesh_ply: 64 -> 39 distinct 128-B lines
+// per ray, L2 misses 1.67 -> 1.21 per ray (model; measured on the GPU:
+// mesh_ply k_trace 9.40 -> 8.95 ms, 681 -> 716 Msamples/s).
+// The world region keeps its preorder layout: an instance or model record
+// returns to the record after it (its return index is also the handle of the
+// hit's container, path.h trav_hit). Placing each instance right before its
+// preorder successor instead was measured (round 3): sphere_grid and
+// cube_field unchanged, Menger 38.1 -> 31.4 Msamples/s (the instance pairs of
+// its leaves end up beside their successors' groups, not their parents').
+struct Relayout {
+  const std::vector<uint32_t>& w;
+  std::vector<uint32_t>& out;
+  std::vector<uint32_t>& remap;
+  uint32_t at = 0;
+
+  void place(uint32_t r) {
+    remap[r] = at;
+    at += rec_slots(w, r);
+  }
+  void group(const std::vector<uint32_t>& g, uint32_t align) {
+    at = (at + align - 1) / align * align;
+    for (uint32_t r : g) place(r);
+  }
+
+  // records [begin .. end_rec] (end_rec: the region's END record) of a region
+  // without instance / model records
+  void region(uint32_t begin, uint32_t end_rec) {
+    std::vector<uint32_t> top, kids;
+    for (uint32_t j = begin; j != end_rec; j = rec_is_box(w, j) ? w[4 * (j + 1) + 2] : rec_next(w, j)) top.push_back(j);
+    std::vector<uint32_t> stack(top.rbegin(), top.rend());
+    std::vector<uint32_t> boxes;  // DFS order
     while (!stack.empty()) {
-      const uint32_t b = stack.back();
+      const uint32_t r = stack.back();
       stack.pop_back();
-      if (!rec_is_box(w, b)) continue;
+      if (rec_kind(w, r) == KIND_INST || rec_kind(w, r) == KIND_MODEL)
+        throw std::logic_error("relayout: an instance inside a relaid region");
+      if (!rec_is_box(w, r)) continue;
+      boxes.push_back(r);
+      box_children(w, r, kids);
+      for (size_t k = kids.size(); k-- > 0;) stack.push_back(kids[k]);
+    }
+    at = (at + 7) & ~7u;  // the region on a 128-B line
+    group(top, 4);
+    for (uint32_t b : boxes) {
       box_children(w, b, kids);
       bool any_box = false;
       for (uint32_t c : kids) any_box |= rec_is_box(w, c);
-      for (size_t k = 0; k < kids.size(); ++k) {
-        order.push_back(kids[k]);
-        group_start.push_back(k ? 0 : (any_box ? 4 : 2));  // slots of alignment
-      }
-      for (size_t k = kids.size(); k-- > 0;)
-        if (rec_is_box(w, kids[k])) stack.push_back(kids[k]);
+      group(kids, any_box ? 4 : 2);
     }
-    order.push_back(r.end);  // END
-    group_start.push_back(2);
-    // positions: the region's root on a 128-B line, groups with a box on
-    // 64 B, groups of primitives only on 32 B (tools/layout_sim.cpp, mesh_ply:
-    // L2 misses per ray 1.29 with 64-B primitive groups, 1.21 with 32-B)
-    uint32_t at = (uint32_t)(out.size() / 4);
-    for (size_t k = 0; k < order.size(); ++k) {
-      if (group_start[k]) at = (at + group_start[k] - 1) / group_start[k] * group_start[k];
-      remap[order[k]] = at;
-      at += rec_slots(w, order[k]);
-    }
+    at = (at + 1) & ~1u;
+    place(end_rec);
+  }
+
+  // copy every placed record of `recs` with its successor indices remapped
+  void emit(const std::vector<uint32_t>& recs) {
     out.resize(4 * (size_t)at, 0u);
-    for (uint32_t o : order) {
-      const uint32_t n = remap[o];
-      const uint32_t sl = rec_slots(w, o);
+    for (uint32_t o : recs) {
+      const uint32_t n = remap[o], sl = rec_slots(w, o);
       std::copy(w.begin() + 4 * (size_t)o, w.begin() + 4 * (size_t)(o + sl), out.begin() + 4 * (size_t)n);
       uint32_t* rec = &out[4 * (size_t)n];
       const uint32_t k = rec_kind(w, o);
@@ -382,24 +393,35 @@ void relayout_blas(HostScene& s) {
         rec[5] = remap[rec[5]];
       }
     }
-    const uint32_t nb = remap[r.begin], ne = remap[r.end];
-    r.begin = nb;
-    r.end = ne;
   }
-  // instance / model records of the world: their BLAS ranges
-  for (uint32_t i : s.rec_starts) {
-    if (i >= first) break;
+};
+
+void relayout(HostScene& s) {
+  const std::vector<uint32_t>& w = s.slots;
+  std::vector<uint32_t> out, remap(w.size() / 4, ~0u);
+  Relayout L{w, out, remap, 0};
+  // the world region (emitted first) as it is
+  uint32_t wend = s.world_end + 2;
+  for (uint32_t i : s.rec_starts)
+    if (i < wend) L.place(i);
+  for (const BlasRegion& r : s.blas_regions) L.region(r.begin, r.end);
+  for (uint32_t i : s.rec_starts)
+    if (remap[i] == ~0u) throw std::logic_error("relayout: a record was not placed");
+  L.emit(s.rec_starts);
+  for (uint32_t i : s.rec_starts) {  // instance / model records: their BLAS ranges
     const uint32_t k = rec_kind(w, i);
     if (k == KIND_INST || k == KIND_MODEL) {
-      out[4 * (size_t)i + 1] = remap[w[4 * (size_t)i + 1]];
-      out[4 * (size_t)i + 2] = remap[w[4 * (size_t)i + 2]];
+      uint32_t* rec = &out[4 * (size_t)remap[i]];
+      rec[1] = remap[rec[1]];
+      rec[2] = remap[rec[2]];
+      if (remap[i + 2] != remap[i] + 2) throw std::logic_error("relayout: an instance moved away from its successor");
     }
   }
-  std::vector<uint32_t> starts;
-  for (uint32_t i : s.rec_starts)
-    starts.push_back(i < first ? i : remap[i]);
-  std::sort(starts.begin(), starts.end());
-  s.rec_starts.swap(starts);
+  s.world_begin = remap[s.world_begin];
+  s.world_end = remap[s.world_end];
+  for (BlasRegion& r : s.blas_regions) r.begin = remap[r.begin], r.end = remap[r.end];
+  for (uint32_t& i : s.rec_starts) i = remap[i];
+  std::sort(s.rec_starts.begin(), s.rec_starts.end());
   s.slots.swap(out);
 }
 
@@ -540,7 +562,7 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
   }
   if (e.mix_alpha) s.trav_rng = true;
   const char* lay = getenv("MRT_LAYOUT");  // "dfs": keep the preorder stream (A/B)
-  if (!(lay && !strcmp(lay, "dfs"))) relayout_blas(s);
+  if (!(lay && !strcmp(lay, "dfs"))) relayout(s);
   if (s.slots.size() / 4 >= kLdsTag) return (err = "scene too large (record stream >= 2^30 slots)", false);
   return true;
 }
