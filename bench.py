@@ -455,6 +455,16 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
                  "launches": int(ks["shade_launches"]), "achieved": round(sb / (sms * 1e-3) / 1e9, 1),
                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(sb / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                  "bytes_per_path": SHADE_BYTES, "paths_per_sample": round(cnt["shaded"] / max(cnt["samples"], 1), 4)}
+        # the same kernel with ONE queue (MRT_QUEUES=1 profile, tools/profile.sh TAG=_solo): alone on the
+        # GPU; in the bench run it shares the CUs with the other queue's k_trace by design
+        pjs = load_pmc(REPO / "profiles" / f"pmc_{scene}_solo.json", stamp)
+        kso = pjs["kernels"].get("k_shade", {}) if pjs else {}
+        if kso.get("hbm_bytes_per_launch") and kso.get("avg_ns"):
+            shade["solo"] = {"pmc": f"profiles/pmc_{scene}_solo.json (src {stamp['src']}, MRT_QUEUES=1)",
+                             "avg_launch_ms": round(kso["avg_ns"] * 1e-6, 4),
+                             "traffic": round(kso["hbm_bytes_per_launch"]),
+                             "achieved": round(kso["hbm_bytes_per_launch"] / kso["avg_ns"], 1),
+                             "frac": round(kso["hbm_bytes_per_launch"] / kso["avg_ns"] / HBM_PEAK_GBS, 4)}
         ksh = pj["kernels"].get("k_shade", {}) if pj else {}
         if ksh.get("hbm_bytes_per_launch"):  # PMC of the same source and config (rocprof's per-launch average)
             shade["traffic"] = round(ksh["hbm_bytes_per_launch"])

@@ -100,6 +100,12 @@ t = summary["kernels"].get("k_trace", {})
 if "hbm_bytes_per_launch" in t:
     summary["k_trace_hbm_bytes_per_launch"] = t["hbm_bytes_per_launch"]
 print(json.dumps(summary, indent=1))
-for dst in (REPO / "profiles" / f"pmc_{scene}.json", out_dir / f"pmc_{scene}.json"):  # out_dir: travels back
+import os  # noqa: E402
+
+tag = os.environ.get("PMC_TAG", "")
+if tag:
+    summary["tag"] = tag
+    summary["env"] = {k: v for k, v in os.environ.items() if k.startswith("MRT_")}
+for dst in (REPO / "profiles" / f"pmc_{scene}{tag}.json", out_dir / f"pmc_{scene}{tag}.json"):  # out_dir: travels back
     dst.write_text(json.dumps(summary, indent=1))
     print("wrote", dst)

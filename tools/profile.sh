@@ -7,7 +7,8 @@
 set -o pipefail
 export TMPDIR=/tmp
 SCENE=${SCENE:-sphere_grid}
-OUT=gpurun_out/prof_$SCENE
+TAG=${TAG:-}   # e.g. TAG=_solo with MRT_QUEUES=1: profiles/pmc_<scene>_solo.json (not read by bench.py)
+OUT=gpurun_out/prof_$SCENE$TAG
 rm -rf $OUT; mkdir -p $OUT
 B="bench.py --scene $SCENE --no-cpu-baseline --no-dropin --secondary none"
 P="--steps 1 --warmup 1 --no-kernel-timing"
@@ -23,5 +24,5 @@ EXTRA="$P" run sq 240 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_R
 EXTRA="$P" run sq2 240 --pmc SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE
 rc=$?
 echo "profile $SCENE rc=$rc"
-[ $rc -eq 0 ] && python3 tools/pmc_summary.py $OUT $SCENE > $OUT/summary.log 2>&1; tail -40 $OUT/summary.log
+[ $rc -eq 0 ] && PMC_TAG=$TAG python3 tools/pmc_summary.py $OUT $SCENE > $OUT/summary.log 2>&1; tail -40 $OUT/summary.log
 exit $rc
