@@ -1780,7 +1780,7 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     c->S = S;
     c->scene_bytes = off;
     c->trace_lds = S.n_tlet > 0;
-    // Persistent-loop thresholds per scene (profiles/r2_tune):
+    // Persistent-loop thresholds per scene (profiles/r2_tune, r3_tune.txt):
     // a record stream larger than half the chip's L2 (32 MiB over 8 XCDs)
     // misses to the Infinity Cache, each load round trip is longer, and it
     // pays to keep more lanes per load instruction (box run while >= 32 lanes
@@ -1788,9 +1788,14 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     // 38.2 Msamples/s; L2-resident streams keep 32/24 (sphere_grid 640 vs
     // 609, cube_field 252 vs 246).
     if (c->tune_auto_loop) {
+      // round 3, after the box run was unrolled (profiles/r3_tune.txt):
+      // refill 32 everywhere; box run while >= 32 lanes are at a box for a
+      // stream past half the L2 (mesh_ply 749 -> 775), >= 16 for an
+      // instance-heavy world (cube_field 266 -> 275), else >= 24 (sphere_grid)
       const bool big = (size_t)S.n_slots * 16 > ((size_t)16 << 20);
-      c->tune.refill = big ? 16u : 32u;
-      c->tune.box_min = big ? 32u : 24u;
+      const bool instanced = S.n_inst > 1000;
+      c->tune.refill = 32u;
+      c->tune.box_min = big ? 32u : (instanced ? 16u : 24u);
     }
     c->tl_boxes = hs.tl_boxes;
     c->scene_alpha = hs.has_alpha;
