@@ -163,7 +163,7 @@ __global__ __launch_bounds__(kBlock) void k_generate(DevCamera cam, RenderParams
 constexpr float kTmin = 0.001f;          // World::intersect(ray, 0.001, INFINITY) (main.rs trace)
 // Scheduling knobs of the persistent loop (kernel arguments so that they can
 // be tuned without a rebuild: MRT_TRACE_REFILL / _PRIM_BATCH / _CHUNK).
-constexpr uint64_t kResultsMax = 256ull << 20;  // samples per results slab (4 GiB)
+constexpr uint64_t kResultsMax = 1ull << 30;  // samples per results slab (16 GiB per queue set)
 
 struct TraceTune {
   uint32_t chunk = 128;     // rays per atomic grab
@@ -923,9 +923,11 @@ struct mrt_ctx {
   // Live paths per iteration (MRT_POOL_PATHS overrides). Large on purpose:
   // every k_trace launch ends with a tail of long rays on few lanes, so the
   // more rays a launch carries the smaller that tail's share (measured on
-  // SphereGrid 1080p: 2M paths 186, 16M 377, 64M 434 Msamples/s). 64M paths
-  // hold 11 GiB of HBM (176 B each).
-  size_t pool_paths = (size_t)128 << 20;
+  // SphereGrid 1080p: 2M paths 186, 16M 377, 64M 434 Msamples/s; round 3,
+  // 256-spp steps: 64M 674, 128M 716, 256M 762, 384M 777, 544M 770). 384M
+  // paths hold 66 GiB of HBM (176 B each); a render allocates
+  // min(samples per chunk, pool_paths).
+  size_t pool_paths = (size_t)384 << 20;
   int cus = 1;
   bool trace_lds = false;          // the scene has an LDS treelet (set per scene)
   bool tune_auto_loop = true;      // refill/box_min chosen per scene (unless MRT_TRACE_REFILL/BOX_MIN set)
@@ -1618,7 +1620,7 @@ int mrt_create(int device, mrt_ctx** out) {
     if (const char* e = getenv("MRT_TRACE_CHUNK")) c->tune.chunk = (uint32_t)std::max(64, atoi(e));
     if (const char* e = getenv("MRT_TRACE_BOX_MIN")) c->tune.box_min = (uint32_t)std::max(1, std::min(65, atoi(e)));
     if (const char* e = getenv("MRT_SHADE_BATCH")) c->tune.shade_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    if (const char* e = getenv("MRT_POOL_PATHS")) c->pool_paths = (size_t)std::max(1 << 16, std::min(1 << 28, atoi(e)));
+    if (const char* e = getenv("MRT_POOL_PATHS")) c->pool_paths = (size_t)std::max(1 << 16, std::min(1 << 30, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_BLOCK")) {
       const int b = atoi(e);
       c->trace_block = b >= 1024 ? 1024 : (b >= 512 ? 512 : 256);

@@ -75,23 +75,23 @@ def textured(assets_dir):
 
 
 def test_4k_pixel_subset_across_result_chunks(ctx, textured):
-    """64 spp of the 4K frame = 531M samples: the library splits them into
-    result-slab chunks (256M samples, i.e. 30 spp of 8.3M pixels), so this
-    crosses two chunk boundaries. A pixel subset must match the oracle
+    """144 spp of the 4K frame = 1.19G samples: the library splits them into
+    result-slab chunks (2^30 samples, i.e. 129 spp of 8.3M pixels), so this
+    crosses a chunk boundary. A pixel subset must match the oracle
     (bounces bit-exact; radiance within 1e-4: acos/atan2 of SkySphere are
     ocml vs glibc ULPs), and splitting the call at the chunk boundary must
     not change a bit."""
     b, o = textured
     ctx.upload(b)
-    spp = 64
+    spp = 144
     rgb, bo = ctx.render(W4, H4, 0, spp, seed=5)
     px = np.arange(3, W4 * H4, 15_013, dtype=np.uint32)
     orgb, obo = o.render_pixels(W4, H4, px, 0, spp, seed=5)
     assert np.array_equal(bo[px], obo)
     a = rgb.reshape(-1, 3)[px].astype(np.float64)
     assert np.linalg.norm(a - orgb.reshape(-1, 3)) / np.linalg.norm(orgb) <= 1e-4
-    part = ctx.render(W4, H4, 0, 30, seed=5)
-    part = ctx.render(W4, H4, 30, spp - 30, seed=5, accum=part)
+    part = ctx.render(W4, H4, 0, 129, seed=5)
+    part = ctx.render(W4, H4, 129, spp - 129, seed=5, accum=part)
     assert np.array_equal(rgb.view(np.uint32), part[0].view(np.uint32)) and np.array_equal(bo, part[1])
 
 

@@ -9,13 +9,13 @@
 #   bash tools/gpu_session.sh configs               # every BASELINE config scene, timing only
 #   LABELS="a b" LIBS="x.so y.so" bash tools/gpu_session.sh ab   # bench per library build (MASSRT_LIB)
 #   SWEEP=$'base\ntl MRT_TREELET_KB=16' bash tools/gpu_session.sh sweep   # bench per env configuration
-# SCENES (default "sphere_grid mesh_ply") and STEPS (default 6) apply to ab / sweep.
+# SCENES (default "sphere_grid mesh_ply") and STEPS (default 3) apply to ab / sweep.
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/session
 MODE=$1; shift
 SCENES=${SCENES:-"sphere_grid mesh_ply"}
-STEPS=${STEPS:-6}
+STEPS=${STEPS:-3}
 
 line() {  # log, label: one summary line of a bench log
   python3 -c "import json,sys; j=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=j['roofline'] or {}; s=j.get('roofline_k_shade') or {}
@@ -39,10 +39,10 @@ case $MODE in
   profile)
     for sc in "$@"; do SCENE=$sc bash tools/profile.sh > gpurun_out/session/profile_$sc.log 2>&1 || exit 1; done ;;
   configs)
-    quick c2_sphere_grid gpurun_out/session/c2.log --scene sphere_grid --steps 8 &&
-    quick c3_cube_field gpurun_out/session/c3.log --scene cube_field --steps 6 &&
-    quick c4_mesh_ply gpurun_out/session/c4p.log --scene mesh_ply --steps 8 &&
-    quick c4_mesh_obj gpurun_out/session/c4o.log --scene mesh_obj --steps 8 &&
+    quick c2_sphere_grid gpurun_out/session/c2.log --scene sphere_grid --steps 4 &&
+    quick c3_cube_field gpurun_out/session/c3.log --scene cube_field --steps 3 &&
+    quick c4_mesh_ply gpurun_out/session/c4p.log --scene mesh_ply --steps 4 &&
+    quick c4_mesh_obj gpurun_out/session/c4o.log --scene mesh_obj --steps 4 &&
     quick c5_mesh_obj_textured_4k gpurun_out/session/c5.log --scene mesh_obj_textured --width 3840 --height 2160 \
       --spp-per-step 16 --total-spp 4096 --steps 6 &&
     quick menger gpurun_out/session/menger.log --scene menger --steps 2 ;;

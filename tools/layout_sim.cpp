@@ -206,6 +206,35 @@ static std::vector<uint32_t> sibling_order(const Stream& s, const Tree& t, uint3
   return out;
 }
 
+// sibling groups, but the groups of the top `levels` levels in BFS order
+// (a contiguous hot treelet), then the remaining groups in DFS order
+static std::vector<uint32_t> sibling_bfs_top(const Stream& s, const Tree& t, uint32_t root, int levels) {
+  std::vector<uint32_t> out{root};
+  std::vector<uint32_t> frontier{root}, deep;
+  for (int l = 0; l < levels && !frontier.empty(); ++l) {
+    std::vector<uint32_t> next;
+    for (uint32_t b : frontier) {
+      auto it = t.kids.find(b);
+      if (it == t.kids.end()) continue;
+      for (uint32_t c : it->second) out.push_back(c);
+      for (uint32_t c : it->second)
+        if (s.box(c)) next.push_back(c);
+    }
+    frontier = next;
+  }
+  std::vector<uint32_t> st(frontier.rbegin(), frontier.rend());
+  while (!st.empty()) {
+    uint32_t b = st.back();
+    st.pop_back();
+    auto it = t.kids.find(b);
+    if (it == t.kids.end()) continue;
+    for (uint32_t c : it->second) out.push_back(c);
+    for (auto c = it->second.rbegin(); c != it->second.rend(); ++c)
+      if (s.box(*c)) st.push_back(*c);
+  }
+  return out;
+}
+
 // hot treelet first: the `hot` boxes of largest surface area (a rooted
 // treelet), BFS order, then every other record in stream order
 static std::vector<uint32_t> hot_first(const Stream& s, const Tree& t, uint32_t root, size_t hot) {
@@ -348,6 +377,8 @@ int main(int argc, char** argv) {
   cands.push_back({"sibling pairs, grp 64, tri 64", pack_groups(s, t, sibling_order(s, t, begin), 64, 64)});
   cands.push_back({"sib, box grp 64, prim grp 16", pack_groups(s, t, sibling_order(s, t, begin), 64, 48, 16)});
   cands.push_back({"sib, box grp 64, prim grp 32", pack_groups(s, t, sibling_order(s, t, begin), 64, 48, 32)});
+  for (int lv : {6, 10, 14})
+    cands.push_back({"sib 64/32, BFS top " + std::to_string(lv), pack_groups(s, t, sibling_bfs_top(s, t, begin, lv), 64, 48, 32)});
   cands.push_back({"sibling pairs, grp 128, tri 64", pack_groups(s, t, sibling_order(s, t, begin), 128, 64)});
   for (size_t hot : {1024, 16384, 131072}) cands.push_back({"hot " + std::to_string(hot) + " first", pack(s, hot_first(s, t, begin, hot), 16)});
   for (int dep : {2, 3, 4}) cands.push_back({"clusters depth " + std::to_string(dep), pack(s, clustered(s, t, begin, dep), 16)});
