@@ -46,7 +46,7 @@ all-logical-cores run; host model and core counts are recorded;
 gpu_over_cpu is against the whole host (host_estimate when the job has a
 CPU quota), gpu_over_cpu_quota<N> against the job's share.
 config.dropin: the Rust binding's render() call pattern (massrt.render:
-pre-pass, clear, num_cpus-2 passes per frame in batches of 64 into the
+pre-pass, clear, num_cpus-2 passes per frame in batches of 256 into the
 device-resident image, a tonemap + host copy per batch), 1080p, both scenes.
 --gpus N without a launcher starts N ranks itself (torch.distributed.run).
 """
@@ -100,7 +100,7 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--pmc-json", default=None, help="PMC summary (default profiles/pmc_<scene>.json)")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in render() call-pattern runs")
-    ap.add_argument("--dropin-batch", type=int, default=64, help="1-spp passes per mrt_image_render call")
+    ap.add_argument("--dropin-batch", type=int, default=256, help="1-spp passes per mrt_image_render call")
     return ap.parse_args()
 
 

@@ -292,14 +292,17 @@ pub struct RenderOptions {
     pub max_depth: u32,
     /// the reference's render thread count; `frame_limit` counts passes per worker
     pub workers: u32,
-    /// 1-spp passes per GPU call (one `update` per batch)
+    /// 1-spp passes per GPU call (one `update` per batch). The default 256
+    /// covers a frame's passes up to 256 workers in one call, so the UI sees
+    /// one update per frame as in main.rs:274-278; bigger calls also keep the
+    /// per-call drain tail small
     pub batch: u32,
     pub prepass: bool,
 }
 
 impl Default for RenderOptions {
     fn default() -> RenderOptions {
-        RenderOptions { max_depth: 50, workers: default_workers(), batch: 64, prepass: true }
+        RenderOptions { max_depth: 50, workers: default_workers(), batch: 256, prepass: true }
     }
 }
 

@@ -768,7 +768,7 @@ def default_workers() -> int:
     return max(1, (os.cpu_count() or 1) - 2)
 
 
-def render(image, streams: SampleStreams, frame_limit=None, workers=None, batch=64, max_depth=MAX_DEPTH,
+def render(image, streams: SampleStreams, frame_limit=None, workers=None, batch=256, max_depth=MAX_DEPTH,
            prepass=True, update=None, keep_going=None) -> int:
     """render(image, event_proxy, world, camera, frame_limit) (main.rs:150-295)
     on the GPU, exactly as bindings/rust/src/lib.rs `render` does it:

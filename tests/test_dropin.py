@@ -110,7 +110,7 @@ def test_rust_render_states_the_same_loop():
              "update(image, passes)"]
     pos = [body.index(s) for s in order]
     assert pos == sorted(pos)
-    assert "(cpus - 2).max(1)" in src and "batch: 64" in src
+    assert "(cpus - 2).max(1)" in src and "batch: 256" in src
     take = src[src.index("pub fn take(&mut self, n: u32)"):]
     assert re.search(r"self.next_sample as u64 \+ n as u64 > u32::MAX as u64", take)
     assert "render_passes" not in src  # the round-2 loop (frame_limit passes in total, fixed seed) is gone
