@@ -27,7 +27,19 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 out_dir = Path(sys.argv[1])
 scene = sys.argv[2] if len(sys.argv) > 2 else "sphere_grid"
-W, H, SPP = (int(x) for x in (sys.argv[3:6] if len(sys.argv) > 5 else (1920, 1080, 64)))
+
+
+def traced_config():
+    """(width, height, spp per step) of the bench line the trace run printed."""
+    lines = (out_dir / "trace.log").read_text().splitlines() if (out_dir / "trace.log").exists() else []
+    for ln in reversed(lines):
+        if ln.startswith("{"):
+            c = json.loads(ln)["config"]
+            return c["width"], c["height"], c["spp_per_step"]
+    raise SystemExit(f"no bench line in {out_dir / 'trace.log'}: pass W H SPP")
+
+
+W, H, SPP = (int(x) for x in sys.argv[3:6]) if len(sys.argv) > 5 else traced_config()
 N_CU, N_XCD = 256, 8
 
 
