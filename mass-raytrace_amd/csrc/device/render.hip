@@ -1791,13 +1791,14 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     // 609, cube_field 252 vs 246).
     if (c->tune_auto_loop) {
       // round 3, after the box run was unrolled (profiles/r3_tune.txt):
-      // refill 32 everywhere; box run while >= 32 lanes are at a box for a
-      // stream past half the L2 (mesh_ply 749 -> 775), >= 16 for an
-      // instance-heavy world (cube_field 266 -> 275), else >= 24 (sphere_grid)
+      // refill 32 everywhere; box run while >= 16 lanes are at a box for an
+      // instance-heavy world (cube_field 266 -> 275, Menger 37.3 -> 44.1),
+      // >= 32 for another stream past half the L2 (mesh_ply 749 -> 775),
+      // else >= 24 (sphere_grid)
       const bool big = (size_t)S.n_slots * 16 > ((size_t)16 << 20);
       const bool instanced = S.n_inst > 1000;
       c->tune.refill = 32u;
-      c->tune.box_min = big ? 32u : (instanced ? 16u : 24u);
+      c->tune.box_min = instanced ? 16u : (big ? 32u : 24u);
     }
     c->tl_boxes = hs.tl_boxes;
     c->scene_alpha = hs.has_alpha;

@@ -44,7 +44,7 @@ case $MODE in
     quick c4_mesh_ply gpurun_out/session/c4p.log --scene mesh_ply --steps 4 &&
     quick c4_mesh_obj gpurun_out/session/c4o.log --scene mesh_obj --steps 4 &&
     quick c5_mesh_obj_textured_4k gpurun_out/session/c5.log --scene mesh_obj_textured --width 3840 --height 2160 \
-      --spp-per-step 16 --total-spp 4096 --steps 6 &&
+      --spp-per-step 64 --total-spp 4096 --steps 2 &&
     quick menger gpurun_out/session/menger.log --scene menger --steps 2 ;;
   ab)
     set -- $LIBS; labels=($LABELS); k=0
