@@ -55,7 +55,10 @@ struct Ctrl {
   uint32_t active[2];
   uint32_t next_work;
   uint32_t shade_short;  // nonzero: a k_shade grid did not cover its live pool (host bound wrong; reported)
-  uint32_t pad_[28];
+  // refill (k_reserve -> k_refill): work items [gen_base, gen_base + gen_count)
+  // go to pool slots [gen_slot, gen_slot + gen_count), behind the survivors
+  uint32_t gen_slot, gen_count, gen_base;
+  uint32_t pad_[25];
   // persistent k_trace work counters (zeroed by k_shade), one 128-B line per
   // XCD group: group g takes its rays from the g-th eighth of the pool
   uint32_t group_next[kGroups * 32];
@@ -156,6 +159,43 @@ __global__ __launch_bounds__(kBlock) void k_generate(DevCamera cam, RenderParams
   out.rng[i] = rs;
 }
 
+// Refill after k_shade compacted the survivors of pool `cur` into the next
+// pool (ctrl->active[cur ^ 1] of them): reserve work items for the free slots
+// behind them from the shared work counter. One thread; the counter is only
+// advanced while it is below G, so it passes G by at most a pool per queue.
+__global__ void k_reserve(Ctrl* ctrl, uint32_t cur, uint32_t* work, uint32_t G, uint32_t cap) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint32_t n = ctrl->active[cur ^ 1];
+  const uint32_t want = n < cap ? cap - n : 0u;
+  uint32_t m = 0, base = G;
+  if (want && __hip_atomic_load(work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G) {
+    base = atomicAdd(work, want);
+    m = base < G ? (G - base < want ? G - base : want) : 0u;
+  }
+  ctrl->gen_slot = n;
+  ctrl->gen_count = m;
+  ctrl->gen_base = base;
+  ctrl->active[cur ^ 1] = n + m;
+}
+
+// ... and generate them (camera rays of consecutive work items, i.e. pixel
+// order): the next k_trace finds the new paths together behind the
+// survivors instead of scattered among them one per finished slot.
+__global__ __launch_bounds__(kBlock) void k_refill(DevCamera cam, RenderParams rp, PathBufs out, const Ctrl* ctrl) {
+  const uint32_t m = ctrl->gen_count, slot = ctrl->gen_slot, base = ctrl->gen_base;
+  for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < m; j += gridDim.x * kBlock) {
+    float4 ro, rd;
+    uint4 rs;
+    gen_work(cam, rp, base + j, ro, rd, rs);
+    const uint32_t i = slot + j;
+    out.ro[i] = ro;
+    out.rd[i] = rd;
+    out.thr[i] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+    out.rad[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    out.rng[i] = rs;
+  }
+}
+
 // Persistent closest-hit kernel: a fixed grid of waves pulls chunks of rays
 // from a counter; inside a wave a lane whose ray has finished takes the next
 // ray of the wave's chunk as soon as enough lanes are idle, so the SIMD keeps
@@ -163,7 +203,9 @@ __global__ __launch_bounds__(kBlock) void k_generate(DevCamera cam, RenderParams
 constexpr float kTmin = 0.001f;          // World::intersect(ray, 0.001, INFINITY) (main.rs trace)
 // Scheduling knobs of the persistent loop (kernel arguments so that they can
 // be tuned without a rebuild: MRT_TRACE_REFILL / _PRIM_BATCH / _CHUNK).
-constexpr uint64_t kResultsMax = 1ull << 30;  // samples per results slab (16 GiB per queue set)
+// samples per results slab at most (16 B each, one slab per queue set):
+// mrt_ctx::results_max, 2^31 = 32 GiB by default (MRT_RESULTS_LOG2 overrides)
+constexpr uint64_t kResultsMaxLimit = 1ull << 31;
 
 struct TraceTune {
   uint32_t chunk = 128;     // rays per atomic grab
@@ -943,6 +985,11 @@ struct mrt_ctx {
   // (MRT_FINISH_PATHS; 0 = never). 500k measured best (profiles/r2_experiments/
   // finish_sweep.txt): mesh_ply 545 -> 678, sphere_grid 638 -> 642 Msamples/s
   uint32_t finish_paths = 500000;
+  // new camera rays: generated by k_reserve + k_refill behind the compacted
+  // survivors (true), or by k_shade into each finished slot (MRT_REFILL_KERNEL=0)
+  bool refill_kernel = true;
+  uint32_t refill_grid = 2048;  // k_refill workgroups (grid-stride; cus * 8)
+  uint64_t results_max = kResultsMaxLimit;  // samples per results slab (MRT_RESULTS_LOG2: 10..31)
   uint32_t finish_grid_div = 1;  // the finish launch takes 1/div of its occupancy grid (MRT_FINISH_GRID_DIV)
 
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t*, uint32_t>> pixlists;
@@ -1335,8 +1382,8 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
   const uint32_t n_pix = pl.second;
   if (n_pix == 0) return;
   const bool count = (a->flags & MRT_RENDER_COUNTERS) != 0;
-  // results slab <= kResultsMax samples (16 B each); pool <= c->pool_paths
-  uint32_t spp_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(a->spp_count, kResultsMax / n_pix));
+  // results slab <= c->results_max samples (16 B each); pool <= c->pool_paths
+  uint32_t spp_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(a->spp_count, c->results_max / n_pix));
   if ((a->flags & MRT_RENDER_SIMPLE_TRACE) && c->scene_ext)
     throw ApiError{MRT_ERR_INVALID, "MRT_RENDER_SIMPLE_TRACE does not support composite surfaces or CubeMap backgrounds"};
   if ((a->flags & MRT_RENDER_FUSED) && !(a->flags & MRT_RENDER_SIMPLE_TRACE)) {
@@ -1456,10 +1503,16 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
             auto* shade = count ? (c->scene_ext ? k_shade<true, true> : k_shade<true, false>)
                                 : (c->scene_ext ? k_shade<false, true> : k_shade<false, false>);
             hipLaunchKernelGGL(shade, dim3(shade_grid(q, L.bound)), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, q.bufs[cur],
-                               q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, L.exhausted ? nullptr : work, res,
-                               c->d_cnt);
+                               q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur,
+                               (L.exhausted || c->refill_kernel) ? nullptr : work, res, c->d_cnt);
           }
           HIP_CHECK(hipGetLastError());
+          if (c->refill_kernel && !L.exhausted) {  // new paths behind the survivors
+            hipLaunchKernelGGL(k_reserve, dim3(1), dim3(64), 0, q.stream, q.ctrl, cur, work, rp.G, rp.pool_cap);
+            hipLaunchKernelGGL(k_refill, dim3(c->refill_grid), dim3(kBlock), 0, q.stream, c->cam, rp, q.bufs[cur ^ 1],
+                               (const Ctrl*)q.ctrl);
+            HIP_CHECK(hipGetLastError());
+          }
           if (timing) {
             m[2] = next_event();
             HIP_CHECK(hipEventRecord(m[2], q.stream));
@@ -1613,6 +1666,9 @@ int mrt_create(int device, mrt_ctx** out) {
     c->cus = std::max(1, cus);
     c->trace_grid = (uint32_t)c->cus * 4;  // k_trace_simple (debug)
     if (const char* e = getenv("MRT_FINISH_PATHS")) c->finish_paths = (uint32_t)std::max(0L, atol(e));
+    c->refill_grid = (uint32_t)c->cus * 8;
+    if (const char* e = getenv("MRT_REFILL_KERNEL")) c->refill_kernel = atoi(e) != 0;
+    if (const char* e = getenv("MRT_RESULTS_LOG2")) c->results_max = 1ull << std::max(10, std::min(31, atoi(e)));
     if (const char* e = getenv("MRT_FINISH_GRID_DIV")) c->finish_grid_div = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (getenv("MRT_TRACE_REFILL") || getenv("MRT_TRACE_BOX_MIN")) c->tune_auto_loop = false;
     if (const char* e = getenv("MRT_TRACE_REFILL")) c->tune.refill = (uint32_t)std::max(1, std::min(64, atoi(e)));

@@ -237,7 +237,9 @@ void ply_skip(Reader& r, PlyFormat fmt, PlyType t) {
     return;
   }
   unsigned char tmp[8];
-  r.read_exact(tmp, type_size(t));
+  const size_t n = type_size(t);
+  if (n > sizeof tmp) throw Error(MRT_ERR_IO, "ply: invalid type");
+  r.read_exact(tmp, n);
 }
 
 }  // namespace

@@ -74,25 +74,39 @@ def textured(assets_dir):
             oracle.Scene(1).builtin("mesh_obj_textured", ASPECT, assets_dir))
 
 
-def test_4k_pixel_subset_across_result_chunks(ctx, textured):
-    """144 spp of the 4K frame = 1.19G samples: the library splits them into
-    result-slab chunks (2^30 samples, i.e. 129 spp of 8.3M pixels), so this
-    crosses a chunk boundary. A pixel subset must match the oracle
-    (bounces bit-exact; radiance within 1e-4: acos/atan2 of SkySphere are
-    ocml vs glibc ULPs), and splitting the call at the chunk boundary must
-    not change a bit."""
+def test_4k_pixel_subset_across_result_chunks(monkeypatch, textured):
+    """144 spp of the 4K frame = 1.19G samples. The results slab holds 2^31
+    samples by default (258 spp of 8.3M pixels); with MRT_RESULTS_LOG2=30 the
+    library splits this call into chunks of 2^30 samples (129 spp), so it
+    crosses a chunk boundary. A pixel subset must match the oracle (bounces
+    bit-exact; radiance within 1e-4: acos/atan2 of SkySphere are ocml vs
+    glibc ULPs), splitting the call at the chunk boundary must not change a
+    bit, and neither must the default slab (one chunk)."""
     b, o = textured
-    ctx.upload(b)
     spp = 144
-    rgb, bo = ctx.render(W4, H4, 0, spp, seed=5)
+    monkeypatch.setenv("MRT_RESULTS_LOG2", "30")
+    c = massrt.Context(0)
+    try:
+        c.upload(b)
+        rgb, bo = c.render(W4, H4, 0, spp, seed=5)
+        part = c.render(W4, H4, 0, 129, seed=5)
+        part = c.render(W4, H4, 129, spp - 129, seed=5, accum=part)
+    finally:
+        c.close()
+    monkeypatch.delenv("MRT_RESULTS_LOG2")
     px = np.arange(3, W4 * H4, 15_013, dtype=np.uint32)
     orgb, obo = o.render_pixels(W4, H4, px, 0, spp, seed=5)
     assert np.array_equal(bo[px], obo)
     a = rgb.reshape(-1, 3)[px].astype(np.float64)
     assert np.linalg.norm(a - orgb.reshape(-1, 3)) / np.linalg.norm(orgb) <= 1e-4
-    part = ctx.render(W4, H4, 0, 129, seed=5)
-    part = ctx.render(W4, H4, 129, spp - 129, seed=5, accum=part)
     assert np.array_equal(rgb.view(np.uint32), part[0].view(np.uint32)) and np.array_equal(bo, part[1])
+    c = massrt.Context(0)
+    try:
+        c.upload(b)
+        whole = c.render(W4, H4, 0, spp, seed=5)
+    finally:
+        c.close()
+    assert np.array_equal(rgb.view(np.uint32), whole[0].view(np.uint32)) and np.array_equal(bo, whole[1])
 
 
 def test_4k_deterministic_and_shard_additive(ctx, textured):

@@ -9,7 +9,8 @@
 #   bash tools/gpu_session.sh configs               # every BASELINE config scene, timing only
 #   LABELS="a b" LIBS="x.so y.so" bash tools/gpu_session.sh ab   # bench per library build (MASSRT_LIB)
 #   SWEEP=$'base\ntl MRT_TREELET_KB=16' bash tools/gpu_session.sh sweep   # bench per env configuration
-# SCENES (default "sphere_grid mesh_ply") and STEPS (default 3) apply to ab / sweep.
+# SCENES (default "sphere_grid mesh_ply") and STEPS (default 3) apply to ab / sweep / args;
+# BENCH_ARGS (e.g. "--spp-per-step 1024") is appended to every sweep run.
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/session
@@ -61,9 +62,17 @@ case $MODE in
       for sc in $SCENES; do
         log=gpurun_out/session/sweep_${lab}_$sc.log
         env "$@" timeout -k 10 400 python bench.py --scene $sc --secondary none --no-cpu-baseline --no-dropin \
-          --steps $STEPS > $log 2>&1 || { echo "FAILED $lab $sc"; tail -5 $log; exit 1; }
+          --steps $STEPS $BENCH_ARGS > $log 2>&1 || { echo "FAILED $lab $sc"; tail -5 $log; exit 1; }
         line $log $lab
       done
     done <<< "$SWEEP" ;;
+  args)  # ARGSETS=$'s256 --spp-per-step 256\ns1k --spp-per-step 1024 --steps 1': bench per argument set
+    while IFS= read -r cfg; do
+      [ -z "$cfg" ] && continue
+      set -- $cfg; lab=$1; shift
+      for sc in $SCENES; do
+        quick "$lab" gpurun_out/session/args_${lab}_$sc.log --scene $sc --steps $STEPS "$@" || exit 1
+      done
+    done <<< "$ARGSETS" ;;
   *) echo "unknown mode $MODE"; exit 2 ;;
 esac
