@@ -6,17 +6,17 @@ in the same invocation, north_star's target scene (config 4's 1M-triangle
 binary PLY mesh, `mesh_ply`) as `config.secondary`.
 
 A step = one pass of the hot path over one batch: `--spp-per-step` x N
-samples (default 256 x N) of every pixel of the 1920x1080 frame; at N=1, 4
-steps = the full 1024-spp config. With N GPUs (torchrun, one rank per GPU,
+samples (default 1024 x N) of every pixel of the 1920x1080 frame; at N=1 a
+step is the whole 1024-spp config frame. With N GPUs (torchrun, one rank per GPU,
 RCCL over xGMI) each rank renders every N-th 8x8 framebuffer tile of the same
 frame, accumulating its tiles in its own HBM frame, and after every step each
 rank's tile slab is gathered onto rank 0 (massrt/shard.py; Image::merge,
 main.rs:629-638) — bit-identical to the 1-GPU image; no other exchange
-exists. Each rank's work per step is fixed (2.07M/N pixels x 256N spp =
-530.8M samples, one results-slab chunk): "weak" scaling — every render call
+exists. Each rank's work per step is fixed (2.07M/N pixels x 1024N spp =
+2.12G samples, one results-slab chunk): "weak" scaling — every render call
 ends in a drain tail (the last paths finish on a nearly idle GPU), so a rank
 needs that much work per call to keep the tail small.
-`--strong` keeps 256 spp per step for any N instead.
+`--strong` keeps 1024 spp per step for any N instead.
 
 Inputs (scene, BVH, camera) are resident in HBM before timing; the
 accumulation buffers live in HBM. `value` = all samples of all ranks / the
@@ -81,12 +81,12 @@ SHADE_BYTES = 5 * 16 + 16 + 5 * 16
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", default="sphere_grid")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp-per-step", type=int, default=256, help="per GPU (x N frame spp per step) unless --strong")
+    ap.add_argument("--spp-per-step", type=int, default=1024, help="per GPU (x N frame spp per step) unless --strong")
     ap.add_argument("--strong", action="store_true", help="fixed spp per step for any N (strong scaling)")
     ap.add_argument("--total-spp", type=int, default=1024, help="spp of the config (reporting only)")
     ap.add_argument("--max-depth", type=int, default=50)
@@ -95,7 +95,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--secondary", default="mesh_ply", help="second scene of the same run ('' or 'none': off)")
-    ap.add_argument("--secondary-steps", type=int, default=4)
+    ap.add_argument("--secondary-steps", type=int, default=2)
     ap.add_argument("--fused", action="store_true", help="one persistent k_render instead of the k_trace/k_shade loop")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--pmc-json", default=None, help="PMC summary (default profiles/pmc_<scene>.json)")

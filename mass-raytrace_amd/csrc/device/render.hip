@@ -66,8 +66,18 @@ struct Ctrl {
 
 // SoA path state, 5 x 16 B per slot:
 //   ro  = {o.x, o.y, o.z, work index g}    rd  = {d.x, d.y, d.z, bounces k}
-//   thr = {T.x, T.y, T.z, -}               rad = {L.x, L.y, L.z, -}
+//   thr = {T.x, T.y, T.z, kHoldsL or 0}    rad = {L.x, L.y, L.z, -}
 //   rng = xoroshiro128** {s0.lo, s0.hi, s1.lo, s1.hi}
+// rad is read and written only while thr.w says the path holds radiance
+// (some component of L has nonzero bits): a path gains L only where a hit
+// both emits and scatters (a Mix of DiffuseLight and a scattering material)
+// — most paths end where they first gain it — so the slot's rad is
+// otherwise stale and L is +0.
+constexpr uint32_t kHoldsL = 1u;
+__device__ __forceinline__ bool holds_l(const float4& thr) { return __float_as_uint(thr.w) != 0u; }
+__device__ __forceinline__ bool nonzero_bits(float x, float y, float z) {
+  return (__float_as_uint(x) | __float_as_uint(y) | __float_as_uint(z)) != 0u;
+}
 struct PathBufs {
   float4* ro;
   float4* rd;
@@ -154,9 +164,28 @@ __global__ __launch_bounds__(kBlock) void k_generate(DevCamera cam, RenderParams
   gen_work(cam, rp, base + i, ro, rd, rs);
   out.ro[i] = ro;
   out.rd[i] = rd;
-  out.thr[i] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-  out.rad[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  out.thr[i] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);  // L = 0: rad not written
   out.rng[i] = rs;
+}
+
+// Lagged status read of a queue (host loop, one per batch): the fields the
+// host needs, written by one wave straight into pinned host memory. A
+// hipMemcpyAsync to pinned memory ran as a 1024-thread blit kernel, which
+// waited for a CU with 16 free wave slots while both queues' kernels held
+// the chip (12-46 ms per read in the kernel trace, the queue's stream stalled
+// behind it); one wave finds a slot at once.
+struct HostStatus {
+  uint32_t active0, active1, shade_short, work;
+};
+__global__ void k_status(const Ctrl* ctrl, const uint32_t* work, HostStatus* out) {
+  if (threadIdx.x != 0) return;
+  HostStatus h;
+  h.active0 = ctrl->active[0];
+  h.active1 = ctrl->active[1];
+  h.shade_short = ctrl->shade_short;
+  h.work = *work;
+  *out = h;
+  __threadfence_system();
 }
 
 // Refill after k_shade compacted the survivors of pool `cur` into the next
@@ -190,8 +219,7 @@ __global__ __launch_bounds__(kBlock) void k_refill(DevCamera cam, RenderParams r
     const uint32_t i = slot + j;
     out.ro[i] = ro;
     out.rd[i] = rd;
-    out.thr[i] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-    out.rad[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    out.thr[i] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);  // L = 0: rad not written
     out.rng[i] = rs;
   }
 }
@@ -398,7 +426,11 @@ MRT_DEV bool shade_step(const DevScene& S, uint32_t max_depth, const Hit& h, V3&
   return k < max_depth;  // trace(depth 0) returns (0, 0)
 }
 
-template <bool COUNT, bool EXT>
+// REGEN: finished slots take new work items from `work` here (the
+// MRT_REFILL_KERNEL=0 loop); without it (default: k_reserve + k_refill
+// generate new paths behind the survivors, and once the work counter is
+// exhausted) the regeneration code is not compiled in.
+template <bool COUNT, bool EXT, bool REGEN>
 #ifndef MRT_SHADE_WPE
 #define MRT_SHADE_WPE 8
 #endif
@@ -429,7 +461,7 @@ __global__ __launch_bounds__(kBlock, MRT_SHADE_WPE) void k_shade(DevScene S, Dev
       ro = in.ro[i];
       rd = in.rd[i];
       thr = in.thr[i];
-      rad = in.rad[i];
+      if (holds_l(thr)) rad = in.rad[i];
       rs = in.rng[i];
       const uint4 hv = hits[i];
       Hit h{__uint_as_float(hv.x), hv.y, hv.z};
@@ -442,7 +474,7 @@ __global__ __launch_bounds__(kBlock, MRT_SHADE_WPE) void k_shade(DevScene S, Dev
         alive = true;
         ro = make_float4(o.x, o.y, o.z, __uint_as_float(g));
         rd = make_float4(d.x, d.y, d.z, __uint_as_float(k));
-        thr = make_float4(T.x, T.y, T.z, 0.0f);
+        thr = make_float4(T.x, T.y, T.z, __uint_as_float(nonzero_bits(L.x, L.y, L.z) ? kHoldsL : 0u));
         rad = make_float4(L.x, L.y, L.z, 0.0f);
         rs = make_uint4((uint32_t)rng.s0, (uint32_t)(rng.s0 >> 32), (uint32_t)rng.s1, (uint32_t)(rng.s1 >> 32));
       } else {
@@ -454,16 +486,14 @@ __global__ __launch_bounds__(kBlock, MRT_SHADE_WPE) void k_shade(DevScene S, Dev
     // regenerate finished slots from the work counter and compact survivors
     // into the next pool: one atomic per workgroup for each (same-address
     // atomics from every wave serialise in L2)
-    // (work == nullptr: the host saw the work counter exhausted — no
-    // reservation, and no barrier round or device atomic for it)
+    // (REGEN only; otherwise no reservation, barrier round or device atomic)
     const unsigned long long need_mask = __ballot(need);
-    const uint32_t wbase = work ? wg_reserve(work, (uint32_t)__popcll(need_mask), wave, s_cnt, s_base) : rp.G;
-    if (need) {
+    const uint32_t wbase = REGEN ? wg_reserve(work, (uint32_t)__popcll(need_mask), wave, s_cnt, s_base) : rp.G;
+    if (REGEN && need) {
       uint32_t g = wbase + lane_rank(need_mask);
       if (g < rp.G) {
         gen_work(cam, rp, g, ro, rd, rs);
         thr = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-        rad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         alive = true;
       }
     }
@@ -475,7 +505,7 @@ __global__ __launch_bounds__(kBlock, MRT_SHADE_WPE) void k_shade(DevScene S, Dev
       out.ro[pos] = ro;
       out.rd[pos] = rd;
       out.thr[pos] = thr;
-      out.rad[pos] = rad;
+      if (holds_l(thr)) out.rad[pos] = rad;
       out.rng[pos] = rs;
     }
   }
@@ -533,7 +563,8 @@ __global__ __launch_bounds__(kBlock) void k_render(DevScene S, DevCamera cam, Re
           if (ADOPT) {  // a wavefront path: {o, g} {d, bounces} T L rng (PathBufs)
             ro = pool.ro[w];
             rd = pool.rd[w];
-            const float4 tv = pool.thr[w], lv = pool.rad[w];
+            const float4 tv = pool.thr[w];
+            const float4 lv = holds_l(tv) ? pool.rad[w] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             rs = pool.rng[w];
             g = __float_as_uint(ro.w);
             k = __float_as_uint(rd.w);
@@ -908,6 +939,8 @@ struct Queue {
   Ctrl* ctrl = nullptr;        // device
   Ctrl* h_status = nullptr;    // pinned, 2 slots (lagged status reads)
   uint32_t* h_work = nullptr;  // pinned, 2 slots: snapshots of the shared work counter
+  HostStatus* h_stat = nullptr;  // pinned coherent, 2 slots, written by k_status
+  HostStatus* d_stat = nullptr;  // the same memory as the device addresses it
   hipEvent_t ev[2]{};
   hipEvent_t join = nullptr;
 };
@@ -988,6 +1021,9 @@ struct mrt_ctx {
   // new camera rays: generated by k_reserve + k_refill behind the compacted
   // survivors (true), or by k_shade into each finished slot (MRT_REFILL_KERNEL=0)
   bool refill_kernel = true;
+  // lagged status reads by k_status into pinned coherent memory (true), or by
+  // hipMemcpyAsync (MRT_STATUS_KERNEL=0)
+  bool status_kernel = true;
   uint32_t refill_grid = 2048;  // k_refill workgroups (grid-stride; cus * 8)
   uint64_t results_max = kResultsMaxLimit;  // samples per results slab (MRT_RESULTS_LOG2: 10..31)
   uint32_t finish_grid_div = 1;  // the finish launch takes 1/div of its occupancy grid (MRT_FINISH_GRID_DIV)
@@ -1500,11 +1536,13 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
             HIP_CHECK(hipEventRecord(m[1], q.stream));
           }
           {
-            auto* shade = count ? (c->scene_ext ? k_shade<true, true> : k_shade<true, false>)
-                                : (c->scene_ext ? k_shade<false, true> : k_shade<false, false>);
+            const bool regen = !(L.exhausted || c->refill_kernel);
+            auto* shade = regen ? (count ? (c->scene_ext ? k_shade<true, true, true> : k_shade<true, false, true>)
+                                         : (c->scene_ext ? k_shade<false, true, true> : k_shade<false, false, true>))
+                                : (count ? (c->scene_ext ? k_shade<true, true, false> : k_shade<true, false, false>)
+                                         : (c->scene_ext ? k_shade<false, true, false> : k_shade<false, false, false>));
             hipLaunchKernelGGL(shade, dim3(shade_grid(q, L.bound)), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, q.bufs[cur],
-                               q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur,
-                               (L.exhausted || c->refill_kernel) ? nullptr : work, res, c->d_cnt);
+                               q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, work, res, c->d_cnt);
           }
           HIP_CHECK(hipGetLastError());
           if (c->refill_kernel && !L.exhausted) {  // new paths behind the survivors
@@ -1519,23 +1557,36 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
             marks.push_back(m);
           }
         }
-        HIP_CHECK(hipMemcpyAsync(&q.h_status[L.slot], q.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, q.stream));
-        HIP_CHECK(hipMemcpyAsync(&q.h_work[L.slot], work, 4, hipMemcpyDeviceToHost, q.stream));
+        if (c->status_kernel) {
+          hipLaunchKernelGGL(k_status, dim3(1), dim3(64), 0, q.stream, (const Ctrl*)q.ctrl, (const uint32_t*)work,
+                             q.d_stat + L.slot);
+          HIP_CHECK(hipGetLastError());
+        } else {
+          HIP_CHECK(hipMemcpyAsync(&q.h_status[L.slot], q.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, q.stream));
+          HIP_CHECK(hipMemcpyAsync(&q.h_work[L.slot], work, 4, hipMemcpyDeviceToHost, q.stream));
+        }
         HIP_CHECK(hipEventRecord(q.ev[L.slot], q.stream));
         if (L.pending) {  // the previous batch's status (one batch stays in flight)
           HIP_CHECK(hipEventSynchronize(q.ev[L.slot ^ 1]));
-          const Ctrl& s = q.h_status[L.slot ^ 1];
+          HostStatus s;
+          if (c->status_kernel) {
+            const volatile HostStatus& v = q.h_stat[L.slot ^ 1];  // written by the GPU
+            s = HostStatus{v.active0, v.active1, v.shade_short, v.work};
+          } else {
+            const Ctrl& h = q.h_status[L.slot ^ 1];
+            s = HostStatus{h.active[0], h.active[1], h.shade_short, q.h_work[L.slot ^ 1]};
+          }
           if (s.shade_short)
             throw ApiError{MRT_ERR_HIP, "internal: a k_shade grid was smaller than its live pool (" +
                                             std::to_string(s.shade_short) + " paths)"};
-          if (q.h_work[L.slot ^ 1] >= rp.G) {
-            L.bound = std::min<size_t>(L.bound, s.active[0]);
+          if (s.work >= rp.G) {
+            L.bound = std::min<size_t>(L.bound, s.active0);
             L.exhausted = true;
           }
-          if (q.h_work[L.slot ^ 1] >= rp.G && s.active[0] <= finish_paths) {
+          if (s.work >= rp.G && s.active0 <= finish_paths) {
             // no new work: the paths left (at most as many as that status
             // showed) finish in one fused launch after the batch just queued
-            if (s.active[0] > 0) {
+            if (s.active0 > 0) {
               std::array<hipEvent_t, 2> fm{};
               if (timing) {
                 fm[0] = next_event();
@@ -1639,6 +1690,9 @@ int mrt_create(int device, mrt_ctx** out) {
       HIP_CHECK(hipMalloc(&q.ctrl, sizeof(Ctrl)));
       HIP_CHECK(hipHostMalloc(&q.h_status, 2 * sizeof(Ctrl), hipHostMallocDefault));
       HIP_CHECK(hipHostMalloc(&q.h_work, 2 * sizeof(uint32_t), hipHostMallocDefault));
+      HIP_CHECK(hipHostMalloc(&q.h_stat, 2 * sizeof(HostStatus), hipHostMallocCoherent | hipHostMallocMapped));
+      memset(q.h_stat, 0, 2 * sizeof(HostStatus));
+      HIP_CHECK(hipHostGetDevicePointer((void**)&q.d_stat, q.h_stat, 0));
       HIP_CHECK(hipEventCreateWithFlags(&q.ev[0], hipEventDisableTiming));
       HIP_CHECK(hipEventCreateWithFlags(&q.ev[1], hipEventDisableTiming));
       HIP_CHECK(hipEventCreateWithFlags(&q.join, hipEventDisableTiming));
@@ -1668,6 +1722,7 @@ int mrt_create(int device, mrt_ctx** out) {
     if (const char* e = getenv("MRT_FINISH_PATHS")) c->finish_paths = (uint32_t)std::max(0L, atol(e));
     c->refill_grid = (uint32_t)c->cus * 8;
     if (const char* e = getenv("MRT_REFILL_KERNEL")) c->refill_kernel = atoi(e) != 0;
+    if (const char* e = getenv("MRT_STATUS_KERNEL")) c->status_kernel = atoi(e) != 0;
     if (const char* e = getenv("MRT_RESULTS_LOG2")) c->results_max = 1ull << std::max(10, std::min(31, atoi(e)));
     if (const char* e = getenv("MRT_FINISH_GRID_DIV")) c->finish_grid_div = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (getenv("MRT_TRACE_REFILL") || getenv("MRT_TRACE_BOX_MIN")) c->tune_auto_loop = false;
@@ -1722,6 +1777,7 @@ int mrt_destroy(mrt_ctx* c) {
     hipFree(q.ctrl);
     if (q.h_status) hipHostFree(q.h_status);
     if (q.h_work) hipHostFree(q.h_work);
+    if (q.h_stat) hipHostFree(q.h_stat);
     for (hipEvent_t e : {q.ev[0], q.ev[1], q.join})
       if (e) hipEventDestroy(e);
     if (q.stream) hipStreamDestroy(q.stream);

@@ -40,13 +40,13 @@ case $MODE in
   profile)
     for sc in "$@"; do SCENE=$sc bash tools/profile.sh > gpurun_out/session/profile_$sc.log 2>&1 || exit 1; done ;;
   configs)
-    quick c2_sphere_grid gpurun_out/session/c2.log --scene sphere_grid --steps 4 &&
-    quick c3_cube_field gpurun_out/session/c3.log --scene cube_field --steps 3 &&
-    quick c4_mesh_ply gpurun_out/session/c4p.log --scene mesh_ply --steps 4 &&
-    quick c4_mesh_obj gpurun_out/session/c4o.log --scene mesh_obj --steps 4 &&
+    quick c2_sphere_grid gpurun_out/session/c2.log --scene sphere_grid --steps 2 &&
+    quick c3_cube_field gpurun_out/session/c3.log --scene cube_field --steps 1 &&
+    quick c4_mesh_ply gpurun_out/session/c4p.log --scene mesh_ply --steps 2 &&
+    quick c4_mesh_obj gpurun_out/session/c4o.log --scene mesh_obj --steps 2 &&
     quick c5_mesh_obj_textured_4k gpurun_out/session/c5.log --scene mesh_obj_textured --width 3840 --height 2160 \
-      --spp-per-step 64 --total-spp 4096 --steps 2 &&
-    quick menger gpurun_out/session/menger.log --scene menger --steps 2 ;;
+      --spp-per-step 256 --total-spp 4096 --steps 2 &&
+    quick menger gpurun_out/session/menger.log --scene menger --spp-per-step 256 --steps 1 ;;
   ab)
     set -- $LIBS; labels=($LABELS); k=0
     for lib in "$@"; do
