@@ -1006,6 +1006,7 @@ struct mrt_ctx {
   int cus = 1;
   bool trace_lds = false;          // the scene has an LDS treelet (set per scene)
   bool tune_auto_loop = true;      // refill/box_min chosen per scene (unless MRT_TRACE_REFILL/BOX_MIN set)
+  bool tune_auto_chunk = true;     // rays per grab chosen per scene (unless MRT_TRACE_CHUNK set)
   uint32_t tl_boxes = 0;           // box records in the treelet
   // LDS treelet: off by default. Measured: it removes the
   // global load of a step only when every lane of the wave is in the copy,
@@ -1728,7 +1729,10 @@ int mrt_create(int device, mrt_ctx** out) {
     if (getenv("MRT_TRACE_REFILL") || getenv("MRT_TRACE_BOX_MIN")) c->tune_auto_loop = false;
     if (const char* e = getenv("MRT_TRACE_REFILL")) c->tune.refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_PRIM_BATCH")) c->tune.prim_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    if (const char* e = getenv("MRT_TRACE_CHUNK")) c->tune.chunk = (uint32_t)std::max(64, atoi(e));
+    if (const char* e = getenv("MRT_TRACE_CHUNK")) {
+      c->tune.chunk = (uint32_t)std::max(64, atoi(e));
+      c->tune_auto_chunk = false;
+    }
     if (const char* e = getenv("MRT_TRACE_BOX_MIN")) c->tune.box_min = (uint32_t)std::max(1, std::min(65, atoi(e)));
     if (const char* e = getenv("MRT_SHADE_BATCH")) c->tune.shade_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_POOL_PATHS")) c->pool_paths = (size_t)std::max(1 << 16, std::min(1 << 30, atoi(e)));
@@ -1911,6 +1915,16 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
       const bool instanced = S.n_inst > 1000;
       c->tune.refill = 32u;
       c->tune.box_min = instanced ? 16u : (big ? 32u : 24u);
+    }
+    // Rays per work grab (round 3, profiles/r3_tune2/, 1024-spp steps): an
+    // L2-resident world without many instances runs longer stretches of
+    // neighbouring rays per wave (camera rays sit together behind the
+    // survivors, §4 Refill): sphere_grid 762.8 / 775.0 / 780.3 / 780.6 at
+    // 128 / 256 / 512 / 1024; mesh_ply 897.4 / 893.1 / 877.8 / 841.4 (its
+    // waves then end on longer tails), so big or instanced worlds keep 128.
+    if (c->tune_auto_chunk) {
+      const bool big = (size_t)S.n_slots * 16 > ((size_t)16 << 20);
+      c->tune.chunk = (big || S.n_inst > 1000) ? 128u : 512u;
     }
     c->tl_boxes = hs.tl_boxes;
     c->scene_alpha = hs.has_alpha;
