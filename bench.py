@@ -37,7 +37,7 @@ roofline (dominant kernel k_trace, closest hit):
              hash) matches this run; else null.
   bound    = the unit the PMC counters show busiest (TA/L1 address path, HBM,
              VALU), e.g. "l1/ta" for SphereGrid.
-roofline_k_shade: k_shade (path-state streaming) against HBM, 176 B per
+roofline_k_shade: k_shade (path-state streaming) against HBM, 144 B per
   shaded path, with the PMC traffic/limiter of the same stamped profile.
 cpu_baseline: the oracle's reference-mode restatement (main.rs:159-290
 threading: num_cpus-2 workers rendering whole 1-spp passes) on a stratified
@@ -73,9 +73,10 @@ TRACE_BYTES = {"node_visits": 32, "triangle_tests": 36, "sphere_tests": 16, "ins
 TRACE_RAY_BYTES = 32 + 16  # ray origin+direction read, hit record written
 
 # k_shade's algorithmic bytes per shaded path: the path state
-# read (ro, rd, thr, rad, rng: 5 x 16 B) + its hit record (16 B) and the
-# state written to the next pool (5 x 16 B)
-SHADE_BYTES = 5 * 16 + 16 + 5 * 16
+# read (ro, rd, thr, rng: 4 x 16 B) + its hit record (16 B) and the state
+# written to the next pool (4 x 16 B); rad moves only for the rare path that
+# holds radiance (a Mix that emits and scatters), so it is not counted
+SHADE_BYTES = 4 * 16 + 16 + 4 * 16
 
 
 def parse():

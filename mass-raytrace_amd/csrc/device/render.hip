@@ -430,11 +430,14 @@ MRT_DEV bool shade_step(const DevScene& S, uint32_t max_depth, const Hit& h, V3&
 // MRT_REFILL_KERNEL=0 loop); without it (default: k_reserve + k_refill
 // generate new paths behind the survivors, and once the work counter is
 // exhausted) the regeneration code is not compiled in.
-template <bool COUNT, bool EXT, bool REGEN>
-#ifndef MRT_SHADE_WPE
-#define MRT_SHADE_WPE 8
-#endif
-__global__ __launch_bounds__(kBlock, MRT_SHADE_WPE) void k_shade(DevScene S, DevCamera cam, RenderParams rp, PathBufs in,
+// WPE: waves per SIMD the register budget is sized for (8: 64 VGPRs, 32 B of
+// scratch; 7: 71 VGPRs, none). With 8, k_shade takes more of the CU beside
+// the other queue's k_trace; a world whose records stream from the Infinity
+// Cache runs better with 7 (mesh_ply 948.6 -> 969.0, 6: 962.9 Msamples/s),
+// an L2-resident one with 8 (sphere_grid 808.8, 7: 778.1, 6: 761.0;
+// profiles/r3_tune2/wpe.txt).
+template <bool COUNT, bool EXT, bool REGEN, int WPE>
+__global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, DevCamera cam, RenderParams rp, PathBufs in,
                                                   PathBufs out, const uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   uint32_t* work, float4* results, DevCounters* cnt) {
   const uint32_t n = ctrl->active[cur];
@@ -1007,6 +1010,8 @@ struct mrt_ctx {
   bool trace_lds = false;          // the scene has an LDS treelet (set per scene)
   bool tune_auto_loop = true;      // refill/box_min chosen per scene (unless MRT_TRACE_REFILL/BOX_MIN set)
   bool tune_auto_chunk = true;     // rays per grab chosen per scene (unless MRT_TRACE_CHUNK set)
+  int shade_wpe = 8;               // k_shade register budget: 8 or 7 waves/SIMD (per scene; MRT_SHADE_WPE)
+  bool shade_wpe_auto = true;
   uint32_t tl_boxes = 0;           // box records in the treelet
   // LDS treelet: off by default. Measured: it removes the
   // global load of a step only when every lane of the wave is in the copy,
@@ -1538,10 +1543,14 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
           }
           {
             const bool regen = !(L.exhausted || c->refill_kernel);
-            auto* shade = regen ? (count ? (c->scene_ext ? k_shade<true, true, true> : k_shade<true, false, true>)
-                                         : (c->scene_ext ? k_shade<false, true, true> : k_shade<false, false, true>))
-                                : (count ? (c->scene_ext ? k_shade<true, true, false> : k_shade<true, false, false>)
-                                         : (c->scene_ext ? k_shade<false, true, false> : k_shade<false, false, false>));
+            auto* shade =
+                regen ? (count ? (c->scene_ext ? k_shade<true, true, true, 8> : k_shade<true, false, true, 8>)
+                               : (c->scene_ext ? k_shade<false, true, true, 8> : k_shade<false, false, true, 8>))
+                : c->shade_wpe == 7
+                    ? (count ? (c->scene_ext ? k_shade<true, true, false, 7> : k_shade<true, false, false, 7>)
+                             : (c->scene_ext ? k_shade<false, true, false, 7> : k_shade<false, false, false, 7>))
+                    : (count ? (c->scene_ext ? k_shade<true, true, false, 8> : k_shade<true, false, false, 8>)
+                             : (c->scene_ext ? k_shade<false, true, false, 8> : k_shade<false, false, false, 8>));
             hipLaunchKernelGGL(shade, dim3(shade_grid(q, L.bound)), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, q.bufs[cur],
                                q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, work, res, c->d_cnt);
           }
@@ -1729,6 +1738,10 @@ int mrt_create(int device, mrt_ctx** out) {
     if (getenv("MRT_TRACE_REFILL") || getenv("MRT_TRACE_BOX_MIN")) c->tune_auto_loop = false;
     if (const char* e = getenv("MRT_TRACE_REFILL")) c->tune.refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("MRT_TRACE_PRIM_BATCH")) c->tune.prim_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
+    if (const char* e = getenv("MRT_SHADE_WPE")) {
+      c->shade_wpe = atoi(e) == 7 ? 7 : 8;
+      c->shade_wpe_auto = false;
+    }
     if (const char* e = getenv("MRT_TRACE_CHUNK")) {
       c->tune.chunk = (uint32_t)std::max(64, atoi(e));
       c->tune_auto_chunk = false;
@@ -1926,6 +1939,8 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
       const bool big = (size_t)S.n_slots * 16 > ((size_t)16 << 20);
       c->tune.chunk = (big || S.n_inst > 1000) ? 128u : 512u;
     }
+    if (c->shade_wpe_auto)  // 7 measured on mesh_ply only: instanced worlds keep 8
+      c->shade_wpe = ((size_t)S.n_slots * 16 > ((size_t)16 << 20) && S.n_inst <= 1000) ? 7 : 8;
     c->tl_boxes = hs.tl_boxes;
     c->scene_alpha = hs.has_alpha;
     c->scene_rng = hs.trav_rng;
