@@ -9,6 +9,7 @@
 #   bash tools/gpu_session.sh configs               # every BASELINE config scene, timing only
 #   LABELS="a b" LIBS="x.so y.so" bash tools/gpu_session.sh ab   # bench per library build (MASSRT_LIB)
 #   SWEEP=$'base\ntl MRT_TREELET_KB=16' bash tools/gpu_session.sh sweep   # bench per env configuration
+#   bash tools/gpu_session.sh rehearse              # bench.py --gpus 2 (gloo) on one GPU
 # SCENES (default "sphere_grid mesh_ply") and STEPS (default 3) apply to ab / sweep / args;
 # BENCH_ARGS (e.g. "--spp-per-step 1024") is appended to every sweep run.
 set -o pipefail
@@ -74,5 +75,9 @@ case $MODE in
         quick "$lab" gpurun_out/session/args_${lab}_$sc.log --scene $sc --steps $STEPS "$@" || exit 1
       done
     done <<< "$ARGSETS" ;;
+  rehearse)  # N>1 without a launcher on the 1-GPU box: both ranks on device 0, gloo staging the slabs
+    MRT_POOL_PATHS=134217728 timeout -k 10 600 python -u bench.py --gpus 2 --dist-backend gloo --spp-per-step 256 \
+      --steps 2 --secondary none --no-cpu-baseline --no-dropin > gpurun_out/session/rehearse2.log 2>&1 &&
+    tail -1 gpurun_out/session/rehearse2.log | cut -c1-400 ;;
   *) echo "unknown mode $MODE"; exit 2 ;;
 esac
