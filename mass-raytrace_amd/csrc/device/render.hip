@@ -91,7 +91,8 @@ struct RenderParams {
   unsigned long long seed;
   uint32_t max_depth;
   uint32_t n_pix;        // pixels in this shard
-  uint32_t G;            // work items in this chunk = n_pix * samples
+  uint32_t G;            // work items in this chunk = n_pix * spp
+  uint32_t spp;          // samples per pixel in this chunk
   uint32_t sample_base;  // absolute sample index of chunk sample 0
   uint32_t pool_cap;     // path slots per buffer
   const uint32_t* pixlist;
@@ -142,8 +143,11 @@ __device__ void flush_counters(DevCounters* c, const LocalCounters& lc, uint32_t
 
 __device__ __forceinline__ void gen_work(const DevCamera& cam, const RenderParams& rp, uint32_t g, float4& ro,
                                          float4& rd, uint4& rs) {
-  uint32_t s_local = g / rp.n_pix;
-  uint32_t lp = g - s_local * rp.n_pix;
+  // work items run sample-minor: the samples of one pixel are consecutive
+  // (camera rays of a wave nearly equal), and the results slab is laid out
+  // the same way, g = pixel * spp + sample
+  uint32_t lp = g / rp.spp;
+  uint32_t s_local = g - lp * rp.spp;
   uint32_t p = rp.pixlist[lp];  // lp < n_pix by construction (g < G)
   uint32_t y = p / rp.W, x = p - y * rp.W;
   PathRng rng = path_rng(rp.seed, p, rp.sample_base + s_local);
@@ -632,7 +636,7 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(const float4* results, ui
   float r = accum_rgb[3 * (size_t)p], g = accum_rgb[3 * (size_t)p + 1], b = accum_rgb[3 * (size_t)p + 2];
   uint32_t k = accum_bounces[p];
   for (uint32_t s = 0; s < n_samples; ++s) {
-    float4 q = results[(size_t)s * n_pix + lp];
+    float4 q = results[(size_t)lp * n_samples + s];
     r = r + q.x;
     g = g + q.y;
     b = b + q.z;
@@ -1379,6 +1383,7 @@ void render_fused(mrt_ctx* c, const mrt_render_args* a, const uint32_t* pixlist_
     rp.max_depth = a->max_depth;
     rp.n_pix = n_pix;
     rp.G = n_pix * cs;
+    rp.spp = cs;
     rp.sample_base = a->spp_begin + done;
     rp.pixlist = pixlist_d;
     rp.pool_cap = 0;
@@ -1469,6 +1474,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
     rp.max_depth = a->max_depth;
     rp.n_pix = n_pix;
     rp.G = n_pix * cs;
+    rp.spp = cs;
     rp.sample_base = a->spp_begin + done;
     rp.pixlist = pl.first;
     rp.pool_cap = (uint32_t)c->q[0].cap;
