@@ -5,22 +5,29 @@ reference's random-spheres scene) at 1920x1080x1024spp, max depth 50 — plus,
 in the same invocation, north_star's target scene (config 4's 1M-triangle
 binary PLY mesh, `mesh_ply`) as `config.secondary`.
 
-A step = one pass of the hot path over one batch: `--spp-per-step` x N
-samples (default 1024 x N) of every pixel of the 1920x1080 frame; at N=1 a
-step is the whole 1024-spp config frame. With N GPUs (torchrun, one rank per GPU,
-RCCL over xGMI) each rank renders every N-th 8x8 framebuffer tile of the same
-frame, accumulating its tiles in its own HBM frame, and after every step each
-rank's tile slab is gathered onto rank 0 (massrt/shard.py; Image::merge,
-main.rs:629-638) — bit-identical to the 1-GPU image; no other exchange
-exists. Each rank's work per step is fixed (2.07M/N pixels x 1024N spp =
-2.12G samples, one results-slab chunk): "weak" scaling — every render call
-ends in a drain tail (the last paths finish on a nearly idle GPU), so a rank
-needs that much work per call to keep the tail small.
-`--strong` keeps 1024 spp per step for any N instead.
+A step = one pass of the hot path over one batch: `--spp-per-step` (default
+1024) samples of every pixel of the 1920x1080 frame, i.e. the whole
+1024-spp config frame, for ANY number of GPUs ("strong" scaling: BASELINE's
+metric and config 4 fix the frame, 1920x1080x1024 spp, and split it over
+1/2/4/8 GPUs; `--weak` renders 1024 x N spp per step instead).
+
+With N GPUs (`--gpus N`, default mode "multi") ONE process drives all N
+devices through the library's multi-device context — the boundary a Rust
+render() links (mrt_create_multi + mrt_image_*, include/massrt.h; main.rs:
+159-170): every device renders every N-th 8x8 framebuffer tile of the frame
+into its own HBM, one host thread per device, and at the end of every step
+the library gathers the devices' tile slabs onto device 0 (Image::merge,
+main.rs:629-638) with RCCL send/recv over xGMI (peer copies on repeated
+devices, e.g. `--devices 0,0` to rehearse on one GPU) — bit-identical to the
+1-GPU image. Under a launcher (torch.distributed.run --nproc-per-node N)
+rank 0 is that process and ranks 1..N-1 only join the barriers around the
+timed region (they never touch a GPU). `--mode ranks` is the alternative:
+one process per GPU, each rendering its tiles through mrt_render_device on
+torch's stream, slabs gathered with torch.distributed (massrt/shard.py).
 
 Inputs (scene, BVH, camera) are resident in HBM before timing; the
-accumulation buffers live in HBM. `value` = all samples of all ranks / the
-max over ranks of the timed wall time.
+accumulation buffers live in HBM. `value` = all samples rendered / the max
+over ranks of the timed wall time (barrier + device sync on both sides).
 
 roofline (dominant kernel k_trace, closest hit):
   achieved = algorithmic bytes per launch (SURVEY §8d model: 32 B per box,
@@ -87,9 +94,15 @@ def parse():
     ap.add_argument("--scene", default="sphere_grid")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp-per-step", type=int, default=1024, help="per GPU (x N frame spp per step) unless --strong")
-    ap.add_argument("--strong", action="store_true", help="fixed spp per step for any N (strong scaling)")
+    ap.add_argument("--spp-per-step", type=int, default=1024, help="frame spp per step (x N with --weak)")
+    ap.add_argument("--weak", action="store_true", help="spp-per-step x N per step (weak scaling); default strong")
+    ap.add_argument("--mode", choices=("multi", "ranks"), default="multi",
+                    help="multi: one process, one multi-device context (library gather); ranks: a process per GPU")
+    ap.add_argument("--devices", default=None, help="multi mode: device ordinals, e.g. 0,0 to rehearse on one GPU")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="context option (mrt_set_option), repeatable")
     ap.add_argument("--total-spp", type=int, default=1024, help="spp of the config (reporting only)")
+    ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE config 3 / 5 lines (config.c3/c5)")
     ap.add_argument("--max-depth", type=int, default=50)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of each CPU baseline run")
@@ -114,17 +127,18 @@ def src_hash() -> str:
     return h()
 
 
-def launch_plan(gpus: int, env: dict, argv: list, port: int):
-    """How `bench.py --gpus N` runs: None = this process is the (only) rank
-    or one rank of a launcher's job; else the command that starts N ranks
-    (torch.distributed.run, one process per GPU, rendezvous on 127.0.0.1).
-    A launcher's WORLD_SIZE must agree with --gpus."""
+def launch_plan(gpus: int, env: dict, argv: list, port: int, mode: str = "multi"):
+    """How `bench.py --gpus N` runs: None = this process runs in place (the
+    only process, or one rank of a launcher's job); else the command that
+    starts N ranks (mode "ranks": torch.distributed.run, one process per GPU,
+    rendezvous on 127.0.0.1). Mode "multi" never spawns: one process drives
+    every device. A launcher's WORLD_SIZE must agree with --gpus."""
     ws = env.get("WORLD_SIZE")
     if ws is not None:
         if int(ws) != gpus:
             raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {gpus}: the launcher and the flag disagree")
         return None
-    if gpus <= 1:
+    if gpus <= 1 or mode == "multi":
         return None
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
             "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
@@ -319,7 +333,7 @@ def load_pmc(path: Path, stamp: dict):
         pj = json.loads(path.read_text())
     except (OSError, ValueError):
         return None
-    st = pj.get("stamp", {})
+    st = {"n_gpus": 1, **pj.get("stamp", {})}  # profiles are taken on one GPU
     if any(st.get(k) != v for k, v in stamp.items()):
         return None
     return pj
@@ -338,131 +352,224 @@ def limiter(pj: dict, kernel: str = "k_trace"):
     return out
 
 
-def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev, cpu: bool) -> dict:
+def context_options(a) -> dict:
+    """--opt NAME=VALUE (mrt_set_option); MASSRT_OPTIONS adds to them (massrt.env_options)."""
+    out = {}
+    for item in a.opt:
+        k, _, v = item.partition("=")
+        out[k.strip()] = int(v)
+    return out
+
+
+def step_plan(a, n_gpus: int) -> dict:
+    """What one timed step renders with n_gpus GPUs: the whole --spp-per-step
+    frame (strong scaling: BASELINE's 1920x1080x1024spp frame split over the
+    GPUs), or spp-per-step x N with --weak. The workload label names exactly
+    that."""
+    spp = a.spp_per_step * (n_gpus if a.weak else 1)
+    return {"spp_per_step": spp, "samples_per_step": a.width * a.height * spp,
+            "scaling": "weak" if (a.weak and n_gpus > 1) else "strong",
+            "workload": f"{a.scene} {a.width}x{a.height}x{spp}spp per step, max_depth {a.max_depth}"}
+
+
+def device_list(a) -> list:
+    """Multi mode: the devices of the one context (--devices, else 0..N-1)."""
+    if a.devices:
+        devs = [int(x) for x in a.devices.split(",") if x.strip()]
+        if len(devs) != a.gpus:
+            raise SystemExit(f"bench.py: --devices lists {len(devs)} devices but --gpus {a.gpus}")
+        return devs
+    return list(range(a.gpus))
+
+
+class MultiRunner:
+    """One process, one context over `devices` (mrt_create_multi) and a
+    device-resident Image: a step renders the frame's samples on every
+    device (each its tiles) and gathers the tiles onto device 0 (library
+    RCCL send/recv or peer copies) — what a Rust render() over several GPUs
+    calls (bindings/rust/src/lib.rs)."""
+
+    def __init__(self, a, scene, devices):
+        import massrt
+
+        self.a, self.devices, self.W, self.H = a, devices, a.width, a.height
+        self.ctx = massrt.Context(devices=devices, options=context_options(a))
+        t = time.perf_counter()
+        b = massrt.Builder(1).builtin(scene, float(massrt.ASPECT_RATIO), str(asset_dir(scene)))
+        self.ctx.upload(b)
+        b.close()
+        self.t_load = time.perf_counter() - t
+        self.img = massrt.Image(self.ctx, self.W, self.H)
+        self.next_sample = 0
+        self.gathers = (0, 0.0)
+
+    def step(self, spp, counters=False, timing=False):
+        self.img.render(self.a.seed, self.next_sample, spp, self.a.max_depth, counters=counters, time_kernels=timing)
+        self.next_sample += spp
+        self.img.gather()  # Image::merge onto device 0; returns once every device's work has ended
+
+    def sync(self):
+        self.img.gather()
+
+    def reset_gather_stats(self):
+        self.gathers = self.img.gather_stats()
+
+    def gather_stats(self):
+        b, ms = self.img.gather_stats()
+        return b - self.gathers[0], ms - self.gathers[1]
+
+    def mean_bounces(self):
+        _, b, passes = self.img.read()
+        return float(b.astype("float64").sum()) / (self.W * self.H * max(passes, 1))
+
+    def close(self):
+        self.img.close()
+        self.ctx.close()
+
+
+class RankRunner:
+    """--mode ranks: this process renders its tiles on its own GPU through
+    mrt_render_device on torch's stream; slabs gathered with torch.distributed
+    (massrt/shard.py)."""
+
+    def __init__(self, a, scene, rank, world, dev):
+        import torch
+
+        import massrt
+        from massrt.shard import ShardedFrame
+
+        self.a, self.rank, self.world, self.W, self.H = a, rank, world, a.width, a.height
+        self.ctx = massrt.Context(torch.cuda.current_device(), options=context_options(a))
+        t = time.perf_counter()
+        b = massrt.Builder(1).builtin(scene, float(massrt.ASPECT_RATIO), str(asset_dir(scene, rank, world)))
+        self.ctx.upload(b)
+        b.close()
+        self.t_load = time.perf_counter() - t
+        self.frame = ShardedFrame(self.W, self.H, dev, rank, world, ctx=self.ctx)
+        self.stream = torch.cuda.current_stream().cuda_stream
+        self.steps = 0
+
+    def step(self, spp, counters=False, timing=False):
+        import massrt
+
+        def render_into(rgb, bounces, s0, n):
+            args = self.ctx.args(self.W, self.H, s0, n, self.a.seed, self.a.max_depth, self.rank, self.world,
+                                 counters=counters, time_kernels=timing,
+                                 flags=massrt.RENDER_FUSED if self.a.fused else 0)
+            self.ctx.render_device(args, rgb.data_ptr(), bounces.data_ptr(), self.stream)
+
+        self.frame.step(render_into, spp)  # renders this rank's tiles, then gathers the tile slabs onto rank 0
+        self.steps += 1
+
+    def sync(self):
+        import torch
+
+        torch.cuda.synchronize()
+
+    def reset_gather_stats(self):
+        self.frame.gather_ms()
+
+    def gather_stats(self):
+        return self.frame.slab_bytes, self.frame.gather_ms()
+
+    def mean_bounces(self):
+        spp = self.frame.spp
+        return float(self.frame.frame()[1].double().sum().item()) / (self.W * self.H * max(spp, 1))
+
+    def close(self):
+        self.frame.close()
+        self.ctx.close()
+
+
+def timed_region(world, steps_fn, sync_fn, pg_dev=None):
+    """Barrier + device sync on both sides of `steps_fn`; every rank's wall
+    time, and the job's = the slowest rank's."""
     import torch
     import torch.distributed as dist
 
-    import massrt
-    from massrt.shard import ShardedFrame
-
-    W, H = a.width, a.height
-    spp = a.spp_per_step if a.strong else a.spp_per_step * world
-
-    ctx = massrt.Context(torch.cuda.current_device())
-    t_load = time.perf_counter()
-    b = massrt.Builder(1).builtin(scene, float(massrt.ASPECT_RATIO), str(asset_dir(scene, rank, world)))
-    ctx.upload(b)
-    b.close()
-    t_load = time.perf_counter() - t_load
-    frame = ShardedFrame(W, H, dev, rank, world, ctx=ctx)
-    stream = torch.cuda.current_stream().cuda_stream
-
-    def step(counters=False, timing=False):
-        def render_into(rgb, bounces, s0, n):
-            args = ctx.args(W, H, s0, n, a.seed, a.max_depth, rank, world, counters=counters, time_kernels=timing,
-                            flags=massrt.RENDER_FUSED if a.fused else 0)
-            ctx.render_device(args, rgb.data_ptr(), bounces.data_ptr(), stream)
-
-        frame.step(render_into, spp)  # renders this rank's tiles, then gathers the tile slabs onto rank 0
-
-    # warmup; the first warmup step also counts traversal events (statistics
-    # for the algorithmic-bytes model — not part of the timed region)
-    ctx.reset_counters()
-    for k in range(max(1, warmup)):
-        step(counters=(k == 0))
-    torch.cuda.synchronize()
-    cnt = ctx.counters()
-    ctx.reset_kernel_stats()
-    frame.gather_ms()  # drop the warmup publishes
-
-    timing = not a.no_kernel_timing
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync_fn()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step(timing=timing)
-    torch.cuda.synchronize()
+    steps_fn()
+    sync_fn()
     if world > 1:
         dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    gather_ms = frame.gather_ms()
-    per_rank = None
-    if world > 1:  # every rank's wall time and publish time; the job's time is the slowest rank's
-        t = torch.tensor([elapsed, gather_ms], dtype=torch.float64)
-        if a.dist_backend == "nccl":
-            t = t.to(dev)
+    elapsed = time.perf_counter() - t0
+    per_rank = [elapsed]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        if pg_dev is not None:
+            t = t.to(pg_dev)
         parts = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(parts, t)
-        per_rank = [(float(p[0]), float(p[1])) for p in parts]
-        elapsed = max(e for e, _ in per_rank)
-    ks = ctx.kernel_stats()
+        per_rank = [float(p[0]) for p in parts]
+    return max(per_rank), per_rank
 
-    samples_total = W * H * spp * steps
-    value = samples_total / elapsed / 1e6
 
-    roof = None
-    if timing and cnt["samples"] > 0 and ks["trace_launches"] > 0:
-        seg_per_sample = cnt["segments"] / cnt["samples"]
-        bytes_per_seg = (sum(TRACE_BYTES[k] * cnt[k] for k in TRACE_BYTES) / max(cnt["segments"], 1)
-                         + TRACE_RAY_BYTES)
-        segs = seg_per_sample * (samples_total / world)  # this rank's share of the timed samples
-        # traversal launches: k_trace, plus the drain hand-off's fused k_render
-        # launches (render.hip launch_finish_v), which trace the last paths'
-        # segments — their shading time counts too (conservative)
-        fin_ms, fin_n = ks.get("finish_ms", 0.0), int(ks.get("finish_launches", 0))
-        trav_launches = ks["trace_launches"] + fin_n
-        bytes_per_launch = bytes_per_seg * segs / trav_launches
-        avg_ms = (ks["trace_ms"] + fin_ms) / trav_launches
-        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        stamp = {"scene": scene, "width": W, "height": H, "spp_per_step": spp, "src": src_hash()}
-        pmc_path = Path(a.pmc_json) if (a.pmc_json and scene == a.scene) else REPO / "profiles" / f"pmc_{scene}.json"
-        pj = load_pmc(pmc_path, stamp)
-        lim = limiter(pj) if pj else {}
-        traffic = pj["kernels"]["k_trace"].get("hbm_bytes_per_launch") if pj else None
-        bound = "unmeasured (no PMC profile of this source and config)"
-        if lim:  # the busiest unit; none at half its peak: the dependent record loads' latency binds
-            cand = {"l1/ta": lim.get("ta_busy", 0.0), "hbm": lim.get("hbm", 0.0), "valu": lim.get("valu_busy", 0.0)}
-            bound = max(cand, key=cand.get)
-            if cand[bound] < 0.5:
-                bound = "latency (dependent record loads)"
-        roof = {
-            "bound": bound, "achieved": round(achieved, 1), "peak": CACHE_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / CACHE_PEAK_GBS, 4), "traffic": round(traffic) if traffic else None,
-            "peak_source": "record stream is L1/L2-served: L2 36.9 TB/s with L1 reuse, MI355X_MICROARCH.md §L2",
-            "hbm": ({"achieved": round(lim["hbm"] * HBM_PEAK_GBS, 1), "peak": HBM_PEAK_GBS,
-                     "frac": round(lim["hbm"], 4)} if "hbm" in lim else None),
-            "limiter": {k: round(v, 4) for k, v in lim.items()} or None,
-            "pmc": str(pmc_path.relative_to(REPO)) + f" (src {stamp['src']})" if pj else None,
-            "kernel": "k_trace + drain k_render<adopt>", "bytes_per_launch": round(bytes_per_launch),
-            "avg_launch_ms": round(avg_ms, 4), "launches": int(trav_launches),
-            "k_trace": {"launches": int(ks["trace_launches"]),
-                        "avg_launch_ms": round(ks["trace_ms"] / ks["trace_launches"], 4)},
-            "finish": ({"launches": fin_n, "avg_launch_ms": round(fin_ms / fin_n, 4)} if fin_n else None),
-            "achieved_per_step": round(bytes_per_seg * segs / elapsed / 1e9, 1),
-            "bytes_per_segment": round(bytes_per_seg, 1), "segments_per_sample": round(seg_per_sample, 4),
-            "lane_utilisation": round(cnt["lane_steps"] / max(cnt["wave_slots"], 1), 4),
-            # box tests the early slab decision left to the exact test (path.h box_hit_any)
-            "box_exact_frac": round(cnt.get("box_exact", 0) / max(cnt["node_visits"], 1), 5),
-        }
-
+def roofline_for(a, scene, cnt, ks, samples_total, elapsed, n_gpus, plan) -> tuple:
+    """(roofline of k_trace, roofline_k_shade) from the counting warmup step's
+    event counts and the timed steps' HIP-event kernel times."""
+    if not (cnt["samples"] > 0 and ks["trace_launches"] > 0):
+        return None, None
+    seg_per_sample = cnt["segments"] / cnt["samples"]
+    bytes_per_seg = (sum(TRACE_BYTES[k] * cnt[k] for k in TRACE_BYTES) / max(cnt["segments"], 1) + TRACE_RAY_BYTES)
+    segs = seg_per_sample * samples_total  # every device's share of the timed samples (kernel stats sum over them)
+    # traversal launches: k_trace, plus the drain hand-off's fused k_render
+    # launches (render.hip launch_finish_v), which trace the last paths'
+    # segments — their shading time counts too (conservative)
+    fin_ms, fin_n = ks.get("finish_ms", 0.0), int(ks.get("finish_launches", 0))
+    trav_launches = ks["trace_launches"] + fin_n
+    bytes_per_launch = bytes_per_seg * segs / trav_launches
+    avg_ms = (ks["trace_ms"] + fin_ms) / trav_launches
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    stamp = {"scene": scene, "width": a.width, "height": a.height, "spp_per_step": plan["spp_per_step"],
+             "src": src_hash(), "n_gpus": n_gpus}
+    pmc_path = Path(a.pmc_json) if (a.pmc_json and scene == a.scene) else REPO / "profiles" / f"pmc_{scene}.json"
+    pj = load_pmc(pmc_path, stamp)
+    lim = limiter(pj) if pj else {}
+    traffic = pj["kernels"]["k_trace"].get("hbm_bytes_per_launch") if pj else None
+    bound = "unmeasured (no PMC profile of this source and config)"
+    if lim:  # the busiest unit; none at half its peak: the dependent record loads' latency binds
+        cand = {"l1/ta": lim.get("ta_busy", 0.0), "hbm": lim.get("hbm", 0.0), "valu": lim.get("valu_busy", 0.0)}
+        bound = max(cand, key=cand.get)
+        if cand[bound] < 0.5:
+            bound = "latency (dependent record loads)"
+    roof = {
+        "bound": bound, "achieved": round(achieved, 1), "peak": CACHE_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / CACHE_PEAK_GBS, 4), "traffic": round(traffic) if traffic else None,
+        "peak_source": "record stream is L1/L2-served: L2 36.9 TB/s with L1 reuse, MI355X_MICROARCH.md §L2",
+        "hbm": ({"achieved": round(lim["hbm"] * HBM_PEAK_GBS, 1), "peak": HBM_PEAK_GBS,
+                 "frac": round(lim["hbm"], 4)} if "hbm" in lim else None),
+        "limiter": {k: round(v, 4) for k, v in lim.items()} or None,
+        "pmc": str(pmc_path.relative_to(REPO)) + f" (src {stamp['src']})" if pj else None,
+        "kernel": "k_trace + drain k_render<adopt>", "bytes_per_launch": round(bytes_per_launch),
+        "avg_launch_ms": round(avg_ms, 4), "launches": int(trav_launches),
+        "k_trace": {"launches": int(ks["trace_launches"]),
+                    "avg_launch_ms": round(ks["trace_ms"] / ks["trace_launches"], 4)},
+        "finish": ({"launches": fin_n, "avg_launch_ms": round(fin_ms / fin_n, 4)} if fin_n else None),
+        "achieved_per_step": round(bytes_per_seg * segs / elapsed / 1e9, 1),
+        "bytes_per_segment": round(bytes_per_seg, 1), "segments_per_sample": round(seg_per_sample, 4),
+        "lane_utilisation": round(cnt["lane_steps"] / max(cnt["wave_slots"], 1), 4),
+        # box tests the early slab decision left to the exact test (path.h box_hit_any)
+        "box_exact_frac": round(cnt.get("box_exact", 0) / max(cnt["node_visits"], 1), 5),
+    }
     shade = None
-    if timing and cnt.get("shaded") and ks["shade_launches"] > 0 and roof is not None:
+    if cnt.get("shaded") and ks["shade_launches"] > 0:
         # k_shade: HBM-streaming (path state in and out), SHADE_BYTES per shaded path
-        shaded = cnt["shaded"] / max(cnt["samples"], 1) * (samples_total / world)
+        shaded = cnt["shaded"] / max(cnt["samples"], 1) * samples_total
         sb = SHADE_BYTES * shaded / ks["shade_launches"]
         sms = ks["shade_ms"] / ks["shade_launches"]
         shade = {"kernel": "k_shade", "bound": "hbm", "bytes_per_launch": round(sb), "avg_launch_ms": round(sms, 4),
                  "launches": int(ks["shade_launches"]), "achieved": round(sb / (sms * 1e-3) / 1e9, 1),
                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(sb / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                  "bytes_per_path": SHADE_BYTES, "paths_per_sample": round(cnt["shaded"] / max(cnt["samples"], 1), 4)}
-        # the same kernel with ONE queue (MRT_QUEUES=1 profile, tools/profile.sh TAG=_solo): alone on the
+        # the same kernel with ONE queue (option queues=1 profile, tools/profile.sh TAG=_solo): alone on the
         # GPU; in the bench run it shares the CUs with the other queue's k_trace by design
         pjs = load_pmc(REPO / "profiles" / f"pmc_{scene}_solo.json", stamp)
         kso = pjs["kernels"].get("k_shade", {}) if pjs else {}
         if kso.get("hbm_bytes_per_launch") and kso.get("avg_ns"):
-            shade["solo"] = {"pmc": f"profiles/pmc_{scene}_solo.json (src {stamp['src']}, MRT_QUEUES=1)",
+            shade["solo"] = {"pmc": f"profiles/pmc_{scene}_solo.json (src {stamp['src']}, queues=1)",
                              "avg_launch_ms": round(kso["avg_ns"] * 1e-6, 4),
                              "traffic": round(kso["hbm_bytes_per_launch"]),
                              "achieved": round(kso["hbm_bytes_per_launch"] / kso["avg_ns"], 1),
@@ -472,21 +579,81 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
             shade["traffic"] = round(ksh["hbm_bytes_per_launch"])
             shade["pmc_avg_launch_ms"] = round(ksh["avg_ns"] * 1e-6, 4)
             shade["limiter"] = {k: round(v, 4) for k, v in limiter(pj, "k_shade").items()}
+    # north_star asks >= 40% of HBM peak during BVH traversal: the co-run and
+    # solo HBM fractions of k_trace from the stamped PMC profiles, side by side
+    pjt = load_pmc(REPO / "profiles" / f"pmc_{scene}_solo.json", stamp)
+    solo = limiter(pjt).get("hbm") if pjt else None
+    roof["north_star_hbm_traversal"] = {
+        "co_run": round(lim["hbm"], 4) if "hbm" in lim else None, "solo": round(solo, 4) if solo else None,
+        "target": 0.40, "met": bool(lim.get("hbm", 0) >= 0.40 or (solo or 0) >= 0.40),
+        "reason": "the record stream is cache-resident (L1 hit %s, L2 hit %s): traversal reads its algorithmic "
+                  "bytes from L1/L2, which exceed the HBM peak; HBM carries only misses and the path state"
+                  % (round(lim["l1_hit"], 3) if "l1_hit" in lim else "?", round(lim["l2_hit"], 3) if "l2_hit" in lim else "?")}
+    return roof, shade
+
+
+def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev, cpu: bool, devices=None,
+              spp=None, width=None, height=None) -> dict:
+    """Bench one scene: `warmup` untimed steps (the first counts traversal
+    events for the algorithmic-bytes model), then `steps` timed steps."""
+    import copy
+
+    a = copy.copy(a)
+    a.scene = scene
+    if spp is not None:
+        a.spp_per_step = spp
+    if width:
+        a.width, a.height = width, height
+    W, H = a.width, a.height
+    n_gpus = len(devices) if devices is not None else world
+    plan = step_plan(a, n_gpus)
+    spp = plan["spp_per_step"]
+    r = MultiRunner(a, scene, devices) if devices is not None else RankRunner(a, scene, rank, world, dev)
+    for k in range(max(1, warmup)):
+        r.step(spp, counters=(k == 0))
+    r.sync()
+    cnt = r.ctx.counters()
+    r.ctx.reset_kernel_stats()
+    r.reset_gather_stats()  # drop the warmup publishes
+    timing = not a.no_kernel_timing
+    pg_dev = dev if (devices is None and world > 1 and a.dist_backend == "nccl") else None
+
+    def steps_fn():
+        for _ in range(steps):
+            r.step(spp, timing=timing)
+
+    elapsed, per_rank = timed_region(world, steps_fn, r.sync, pg_dev)
+    g_bytes, g_ms = r.gather_stats()
+    ks = r.ctx.kernel_stats()
+    samples_total = W * H * spp * steps
+    value = samples_total / elapsed / 1e6
+    roof, shade = (None, None)
+    if timing:
+        # ranks mode: this rank's share of the samples and its own launches
+        share = samples_total / (world if devices is None else 1)
+        roof, shade = roofline_for(a, scene, cnt, ks, share, elapsed, n_gpus, plan)
     out = {"scene": scene, "value": round(value, 3), "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps,
            "warmup": warmup, "width": W, "height": H, "spp_per_step": spp, "samples_per_step": W * H * spp,
-           "scene_load_s": round(t_load, 2), "roofline": roof, "roofline_k_shade": shade}
-    if world > 1:
-        out["gather"] = {"transport": "RCCL (dist.gather over xGMI)" if a.dist_backend == "nccl" else
-                         f"{a.dist_backend} (host-staged)", "bytes_per_rank_per_step": frame.slab_bytes,
-                         "bytes_to_rank0_per_step": W * H * 16, "ms_per_step_rank0": round(per_rank[0][1] / steps, 3),
-                         "per_rank_ms_per_step": [round(e / steps * 1e3, 3) for e, _ in per_rank],
-                         "per_rank_gather_ms_per_step": [round(g / steps, 3) for _, g in per_rank]}
+           "workload": plan["workload"], "scaling": plan["scaling"], "n_gpus": n_gpus,
+           "scene_load_s": round(r.t_load, 2), "roofline": roof, "roofline_k_shade": shade,
+           "tuning": r.ctx.tuning()}
+    if n_gpus > 1:
+        if devices is not None:
+            out["gather"] = {"path": "one process: mrt_create_multi + mrt_image_render / mrt_image_gather",
+                             "devices": devices, "transport": r.ctx.transport(),
+                             "bytes_to_device0_per_step": round(g_bytes / steps),
+                             "ms_per_step": round(g_ms / steps, 3),
+                             "per_rank_ms_per_step": [round(e / steps * 1e3, 3) for e in per_rank]}
+        else:
+            out["gather"] = {"path": "one process per GPU: mrt_render_device + torch.distributed gather",
+                             "transport": "RCCL (dist.gather over xGMI)" if a.dist_backend == "nccl" else
+                             f"{a.dist_backend} (host-staged)", "bytes_per_rank_per_step": g_bytes,
+                             "bytes_to_rank0_per_step": W * H * 16,
+                             "per_rank_ms_per_step": [round(e / steps * 1e3, 3) for e in per_rank]}
     if rank == 0:
-        out["mean_bounces_per_sample"] = round(
-            float(frame.frame()[1].double().sum().item()) / (W * H * spp * (steps + max(1, warmup))), 4)
+        out["mean_bounces_per_sample"] = round(r.mean_bounces(), 4)
         out["mrays_per_s"] = round(value * roof["segments_per_sample"], 1) if roof else None
-    frame.close()
-    ctx.close()
+    r.close()
     if cpu:
         try:
             out["cpu_baseline"] = cpu_baseline(scene, W, H, a.max_depth, a.cpu_seconds, a.seed)
@@ -505,20 +672,50 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
     return out
 
 
+def idle_rank(world: int, n_scenes: int):
+    """Multi mode under a launcher: ranks 1..N-1 own no GPU work (rank 0's
+    context drives every device); they join each timed region's barriers and
+    report their wall time, so the job's time is still the max over ranks."""
+    for _ in range(n_scenes):
+        timed_region(world, lambda: None, lambda: None)
+
+
+def config_lines(a, rank, world, dev, devices) -> dict:
+    """BASELINE configs 3 and 5 on one GPU, each with
+    its roofline: cube_field 1080p x 1024 spp (one frame per step) and the
+    textured 1M-triangle mesh + environment map at 4K, 256 spp per step (of
+    the config's 4096: 2.12G samples, one results chunk)."""
+    out = {}
+    for key, scene, kw, label in (
+            ("c3", "cube_field", dict(spp=1024), "BASELINE config 3: cube.ply x 10k instances, 1080p x 1024 spp"),
+            ("c5", "mesh_obj_textured", dict(spp=256, width=3840, height=2160),
+             "BASELINE config 5: textured 1M-tri mesh + env map, 4K, 256 of 4096 spp per step")):
+        try:
+            r = run_scene(a, scene, 2 if key == "c5" else 1, 1, rank, world, dev, False, devices, **kw)
+            r["config"] = label
+            out[key] = r
+        except Exception as e:
+            out[key] = {"error": str(e)}
+    return out
+
+
 def main():
     a = parse()
-    # --gpus N without a launcher: start the N ranks ourselves, before anything
-    # here touches a GPU, and exit with their status (rank 0 prints the line)
+    # --gpus N without a launcher in "ranks" mode: start the N ranks ourselves,
+    # before anything here touches a GPU, and exit with their status (rank 0
+    # prints the line). "multi" mode always runs in this process.
     import socket
 
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    cmd = launch_plan(a.gpus, os.environ, sys.argv[1:], port)
+    cmd = launch_plan(a.gpus, os.environ, sys.argv[1:], port, a.mode)
     if cmd is not None:
         import subprocess
 
         sys.exit(subprocess.call(cmd, env=dict(os.environ)))
+
+    import datetime
 
     import torch
     import torch.distributed as dist
@@ -528,31 +725,43 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    multi = a.mode == "multi"
+    devices = device_list(a) if multi else None
+    n_gpus = len(devices) if multi else world
+    secondary = a.secondary if (a.secondary and a.secondary != "none" and a.secondary != a.scene) else None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local % torch.cuda.device_count())
-        dist.init_process_group(a.dist_backend)
-    else:
-        torch.cuda.set_device(0)
+        # multi mode: the launcher's other ranks only join barriers (gloo, no GPU)
+        backend = "gloo" if multi else a.dist_backend
+        if not multi:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group(backend, timeout=datetime.timedelta(hours=2))
+        if multi and rank != 0:
+            idle_rank(world, 1 + (secondary is not None))
+            dist.destroy_process_group()
+            return
+    if rank == 0 or not multi:
+        torch.cuda.init()  # torch's HIP runtime first (tests/conftest.py), then libmassrt
+        if not multi or world == 1:
+            torch.cuda.set_device(0 if multi else (local % torch.cuda.device_count() if world > 1 else 0))
     dev = torch.device("cuda", torch.cuda.current_device())
-    cpu = rank == 0 and world == 1 and not a.no_cpu_baseline
+    solo = n_gpus == 1 and world == 1
+    cpu = rank == 0 and solo and not a.no_cpu_baseline
 
-    head = run_scene(a, a.scene, a.steps, a.warmup, rank, world, dev, cpu)
-    sec = None
-    if a.secondary and a.secondary != "none" and a.secondary != a.scene:
-        sec = run_scene(a, a.secondary, a.secondary_steps, 1, rank, world, dev, cpu)
+    head = run_scene(a, a.scene, a.steps, a.warmup, rank, world, dev, cpu, devices)
+    sec = run_scene(a, secondary, a.secondary_steps, 1, rank, world, dev, cpu, devices) if secondary else None
 
-    dropin = None
-    if rank == 0 and world == 1 and not a.no_dropin:
+    dropin, c1, configs = None, None, None
+    if rank == 0 and solo and not a.no_dropin:
         dropin = {}
-        for sc, ref in ((a.scene, head["value"]), (a.secondary, sec["value"] if sec else None)):
-            if sc and sc != "none":
+        for sc, ref in ((a.scene, head["value"]), (secondary, sec["value"] if sec else None)):
+            if sc:
                 try:
                     dropin[sc] = dropin_run(a, sc, ref)
                 except Exception as e:
                     dropin[sc] = {"error": str(e)}
-
-    c1 = None
+    if rank == 0 and solo and not a.no_configs:
+        configs = config_lines(a, rank, world, dev, devices)
     if cpu:
         try:
             c1 = c1_runs(a)
@@ -560,28 +769,35 @@ def main():
             c1 = {"error": str(e)}
 
     if rank == 0:
+        plan = step_plan(a, n_gpus)
+        if multi:
+            par = (f"one process, one context over {n_gpus} device(s) {devices} (mrt_create_multi), 8x8 tile "
+                   f"shards" + (f" + {head['gather']['transport']} gather onto device 0" if n_gpus > 1 else ""))
+        else:
+            par = f"tile-shard x{world}" + ((" + RCCL gather" if a.dist_backend == "nccl" else
+                                            f" + {a.dist_backend} gather") if world > 1 else "")
         line = {
             "metric": METRIC,
             "value": head["value"],
             "unit": "Msamples/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
-            "scaling": "strong" if (a.strong and world > 1) else "weak",
+            "scaling": plan["scaling"],
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (built-in scene, fixed seeds)",
             "config": {
-                "workload": f"{a.scene} {a.width}x{a.height}x{a.total_spp}spp, max_depth {a.max_depth}",
+                "workload": plan["workload"],
                 "scene": a.scene, "width": a.width, "height": a.height, "spp_per_step": head["spp_per_step"],
                 "samples_per_step": head["samples_per_step"], "max_depth": a.max_depth,
-                "parallelism": f"tile-shard x{world}" + (
-                    (" + RCCL gather" if a.dist_backend == "nccl" else f" + {a.dist_backend} gather") if world > 1 else ""),
+                "parallelism": par, "mode": a.mode,
                 "mean_bounces_per_sample": head.get("mean_bounces_per_sample"),
                 "mrays_per_s": head.get("mrays_per_s"),
                 "scene_load_s": head["scene_load_s"],
+                "tuning": head.get("tuning"),
             },
             "roofline": head["roofline"],
             "cpu_baseline": head.get("cpu_baseline"),
@@ -593,6 +809,8 @@ def main():
             line["config"]["c1"] = c1
         if dropin:
             line["config"]["dropin"] = dropin
+        if configs:
+            line["config"].update(configs)
         if head.get("roofline_k_shade"):
             line["roofline_k_shade"] = head["roofline_k_shade"]
         if head.get("gather"):
@@ -601,8 +819,7 @@ def main():
         line["build"] = {"library": massrt.build_info(), "tree": f"src {tree}",
                          "match": massrt.build_info() == f"src {tree}"}
         if sec:
-            sec["workload"] = f"{sec['scene']} {a.width}x{a.height}x{a.total_spp}spp, max_depth {a.max_depth} " \
-                              f"(north_star target: 1M-triangle binary PLY, BASELINE config 4)"
+            sec["workload"] += " (north_star target: 1M-triangle binary PLY, BASELINE config 4)"
             line["config"]["secondary"] = sec
         print(json.dumps(line), flush=True)
     if world > 1:

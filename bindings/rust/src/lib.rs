@@ -15,7 +15,7 @@
 pub mod sys;
 
 use std::collections::HashMap;
-use std::ffi::CStr;
+use std::ffi::{CStr, CString};
 use sys::*;
 
 /// Error of a massrt call: the status code and `mrt_last_error` text.
@@ -174,6 +174,17 @@ impl Context {
                    out: &mut [u8]) -> Result<(), MrtError> {
         assert!(out.len() >= (w * h * 3) as usize);
         self.check(unsafe { mrt_tonemap(self.raw, w, h, rgb.as_ptr(), bounces.as_ptr(), passes, mode, out.as_mut_ptr()) })
+    }
+
+    /// A tuning option of the context (mrt_set_option; names in massrt.h).
+    pub fn set_option(&mut self, name: &str, value: i64) -> Result<(), MrtError> {
+        let c = CString::new(name).expect("option name without NUL");
+        self.check(unsafe { mrt_set_option(self.raw, c.as_ptr(), value) })
+    }
+
+    /// The gather transport of a multi-device context ("rccl", "peer", ...).
+    pub fn transport(&self) -> String {
+        unsafe { CStr::from_ptr(mrt_context_transport(self.raw)) }.to_string_lossy().into_owned()
     }
 
     pub fn raw(&self) -> *mut mrt_ctx {

@@ -1,4 +1,4 @@
-//! Raw FFI of include/massrt.h, MRT_ABI_VERSION 7.
+//! Raw FFI of include/massrt.h, MRT_ABI_VERSION 8.
 //!
 //! Every struct is `#[repr(C)]` with the header's field order and types;
 //! tests/test_rust_binding.py parses this file and checks each struct's
@@ -8,7 +8,7 @@
 
 use std::os::raw::{c_char, c_void};
 
-pub const MRT_ABI_VERSION: i32 = 7;
+pub const MRT_ABI_VERSION: i32 = 8;
 
 pub const MRT_OK: i32 = 0;
 pub const MRT_ERR_INVALID: i32 = 1;
@@ -277,6 +277,24 @@ pub struct mrt_kernel_stats {
     pub finish_launches: u64,
 }
 
+/// Context options (ABI v8): the gather transport of a multi-device context.
+pub const MRT_GATHER_AUTO: i64 = 0;
+pub const MRT_GATHER_PEER: i64 = 1;
+pub const MRT_GATHER_RCCL: i64 = 2;
+
+/// The tuning in effect after the per-scene rules (mrt_get_tuning).
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct mrt_tuning {
+    pub queues: u32,
+    pub trace_refill: u32,
+    pub trace_box_min: u32,
+    pub trace_chunk: u32,
+    pub shade_waves: u32,
+    pub pool_paths: u64,
+    pub results_max: u64,
+}
+
 /// Opaque handles.
 #[repr(C)]
 pub struct mrt_ctx {
@@ -315,6 +333,9 @@ extern "C" {
     pub fn mrt_debug_build() -> i32;
     pub fn mrt_reset_kernel_stats(ctx: *mut mrt_ctx) -> i32;
     pub fn mrt_scene_device_bytes(ctx: *mut mrt_ctx, out: *mut u64) -> i32;
+    pub fn mrt_set_option(ctx: *mut mrt_ctx, name: *const c_char, value: i64) -> i32;
+    pub fn mrt_get_option(ctx: *mut mrt_ctx, name: *const c_char, value: *mut i64) -> i32;
+    pub fn mrt_get_tuning(ctx: *mut mrt_ctx, out: *mut mrt_tuning) -> i32;
 
     // ---- multi-GPU tile exchange (Image::merge, main.rs:629-638)
     pub fn mrt_shard_pixels(width: u32, height: u32, shard_index: u32, shard_count: u32, pixels: *mut u32,
@@ -329,6 +350,7 @@ extern "C" {
     // ---- one context over several devices (ABI v7)
     pub fn mrt_create_multi(n_devices: i32, devices: *const i32, out: *mut *mut mrt_ctx) -> i32;
     pub fn mrt_context_devices(ctx: *mut mrt_ctx, n_devices: *mut i32, devices: *mut i32) -> i32;
+    pub fn mrt_context_transport(ctx: *const mrt_ctx) -> *const c_char;
 
     // ---- device-resident Image (main.rs:598-638, ABI v7)
     pub fn mrt_image_create(ctx: *mut mrt_ctx, width: u32, height: u32, out: *mut *mut mrt_image) -> i32;
@@ -338,6 +360,7 @@ extern "C" {
         -> i32;
     pub fn mrt_image_prepass(img: *mut mrt_image, seed: u64) -> i32;
     pub fn mrt_image_read(img: *mut mrt_image, rgb: *mut f32, bounces: *mut u32, passes: *mut u32) -> i32;
+    pub fn mrt_image_gather(img: *mut mrt_image) -> i32;
     pub fn mrt_image_tonemap(img: *mut mrt_image, mode: u32, rgb8: *mut u8) -> i32;
     pub fn mrt_image_gather_stats(img: *mut mrt_image, bytes: *mut u64, ms: *mut f64) -> i32;
 

@@ -23,6 +23,8 @@
  *  - a context drives one GPU (mrt_create) or several (mrt_create_multi, one
  *    process); multi-process multi-GPU = one process (rank) per GPU, each
  *    rendering its shard of framebuffer tiles (mrt_render_args.shard_*).
+ *  - tuning comes from the caller (mrt_set_option), never from the process
+ *    environment.
  *
  * The reference's Rust side would bind these with `extern "C"` (see
  * INTEGRATION.md); the C++ host in this repo (mass-raytrace_amd/csrc/host)
@@ -39,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 7
+#define MRT_ABI_VERSION 8
 
 /* ---- status codes ------------------------------------------------------ */
 #define MRT_OK 0
@@ -312,6 +314,41 @@ int mrt_reset_kernel_stats(mrt_ctx* ctx);
 /* bytes of device memory held for the scene */
 int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
 
+/* ---- context options (ABI v8) -------------------------------------------
+ * Tuning of the wavefront loop, per context (on a multi-device context: every
+ * device). Values are integers; -1 where allowed = the per-scene rule chosen
+ * at upload. Unknown names and out-of-range values: MRT_ERR_INVALID.
+ *   queues            1..4   path pools on their own streams (default 2)
+ *   pool_paths        live paths at most (default 384Mi; capped by free memory)
+ *   results_log2      10..31 samples per results slab at most (default 31)
+ *   finish_paths      drain hand-off threshold, 0 = never (default 500000)
+ *   finish_grid_div   1..64  (default 1)
+ *   trace_refill      -1, 1..64  k_trace refill threshold (-1: 32)
+ *   trace_box_min     -1, 1..65  k_trace box-run threshold (-1: per scene)
+ *   trace_chunk       -1, >= 64  rays per work grab (-1: per scene)
+ *   trace_prim_batch  1..64  (default 1)
+ *   trace_wgs_per_cu  0..32  persistent-grid workgroups per CU (0: occupancy)
+ *   shade_waves       -1, 7, 8  k_shade register budget (-1: per scene)
+ *   shade_batch       1..64  fused kernel's shade batch (default 16)
+ *   treelet_kb        0..150 LDS treelet per workgroup (default 0; next upload)
+ *   trace_block       256, 512, 1024  k_trace workgroup beside a treelet
+ *   mem_reserve_mb    device memory a render leaves free (default 4096)
+ *   gather            MRT_GATHER_* (multi-device contexts)
+ * Every render sizes its path pool and results slab to the device memory
+ * free at that moment minus mem_reserve_mb (several contexts may share a
+ * device), shrinking the pool first and then the samples per chunk. */
+#define MRT_GATHER_AUTO 0 /* RCCL between distinct devices, peer copies otherwise */
+#define MRT_GATHER_PEER 1 /* HIP peer copies */
+#define MRT_GATHER_RCCL 2 /* RCCL send/recv (distinct devices only) */
+int mrt_set_option(mrt_ctx* ctx, const char* name, int64_t value);
+int mrt_get_option(mrt_ctx* ctx, const char* name, int64_t* value);
+/* the values in effect after the per-scene rules (devices[0] of a multi-device context) */
+typedef struct {
+  uint32_t queues, trace_refill, trace_box_min, trace_chunk, shade_waves;
+  uint64_t pool_paths, results_max;
+} mrt_tuning;
+int mrt_get_tuning(mrt_ctx* ctx, mrt_tuning* out);
+
 /* ---- multi-GPU tile exchange (Image::merge, main.rs:629-638) ------------
  * A render sharded over N devices (mrt_render_args.shard_index/count) leaves
  * each device's accumulation buffers holding its own tiles only. A shard's
@@ -340,9 +377,12 @@ int mrt_shard_unpack_device(mrt_ctx* ctx, uint32_t width, uint32_t height, uint3
  * over the devices — device i renders shard (shard_index*n + i) of
  * (shard_count*n), one host thread per device — and the devices' slabs are
  * gathered onto devices[0] (RCCL send/recv over xGMI when the devices are
- * distinct, HIP peer copies otherwise; MRT_GATHER=peer|rccl overrides). Every
- * pixel is summed on one device only, so the image equals the one-device
- * render bit for bit.
+ * distinct, HIP peer copies otherwise; option "gather" overrides). With
+ * distinct devices mrt_create_multi opens RCCL and creates its communicators
+ * at once; if that fails the context falls back to peer copies and
+ * mrt_context_transport says why. Every pixel is summed on one device only,
+ * so the image equals the one-device render bit for bit. mrt_render with
+ * host buffers sends each device only its own shard's pixels.
  * On such a context mrt_upload_scene, mrt_set_camera and mrt_render (host
  * buffers) use every device; mrt_get/reset_counters and mrt_get/reset_
  * kernel_stats sum over them; every other entry point runs on devices[0]
@@ -350,6 +390,9 @@ int mrt_shard_unpack_device(mrt_ctx* ctx, uint32_t width, uint32_t height, uint3
 int mrt_create_multi(int n_devices, const int* devices, mrt_ctx** out);
 /* devices the context spans (1 for mrt_create) and their ordinals (may be NULL) */
 int mrt_context_devices(mrt_ctx* ctx, int* n_devices, int* devices);
+/* the gather transport: "none" (one device), "peer", "rccl", or
+ * "peer (...)" with the reason RCCL was not used */
+const char* mrt_context_transport(const mrt_ctx* ctx);
 
 /* ---- device-resident Image (main.rs:598-638, ABI v7) --------------------
  * The reference's Image {pass count, per-pixel (colour sum, depth sum),
@@ -357,7 +400,9 @@ int mrt_context_devices(mrt_ctx* ctx, int* n_devices, int* devices);
  * host round trip, and only a read or a tonemap crosses PCIe — the call
  * pattern of a render() whose passes are batched. On a
  * multi-device context every device keeps the sums of its own tiles and a
- * read gathers them. Calls on one image are serialized by the caller. */
+ * read gathers them. Calls on one image are serialized by the caller.
+ * An image must be destroyed before its context: mrt_destroy returns
+ * MRT_ERR_STATE (and destroys nothing) while images of the context exist. */
 typedef struct mrt_image mrt_image;
 int mrt_image_create(mrt_ctx* ctx, uint32_t width, uint32_t height, mrt_image** out);
 int mrt_image_destroy(mrt_image* img);
@@ -372,8 +417,13 @@ int mrt_image_render(mrt_image* img, uint64_t seed, uint32_t spp_begin, uint32_t
                      uint32_t flags);
 /* Camera::albedo_normal pre-pass into the image (main.rs:162-222; as mrt_prepass) */
 int mrt_image_prepass(mrt_image* img, uint64_t seed);
-/* sums (W*H*3 f32) and depths (W*H u32) — either may be NULL — and the pass count */
+/* sums (W*H*3 f32) and depths (W*H u32) — either may be NULL — and the pass
+ * count; with both NULL only the count is returned (no gather, no sync) */
 int mrt_image_read(mrt_image* img, float* rgb, uint32_t* bounces, uint32_t* passes);
+/* Image::merge of the devices' tiles at the end of a frame: gathers them onto
+ * devices[0] (device-resident, no host copy) and waits until every device's
+ * queued work has ended */
+int mrt_image_gather(mrt_image* img);
 /* Image::to_rgb_bytes + dump's row flip (as mrt_tonemap) on devices[0]: W*H*3
  * bytes, top row first. ALBEDO / NORMAL show the pre-pass (zeros before one). */
 int mrt_image_tonemap(mrt_image* img, uint32_t mode, uint8_t* rgb8);

@@ -81,7 +81,7 @@ const Rccl& rccl() {
     }
   }
   if (!r.comm_init_all || !r.group_start || !r.group_end || !r.send || !r.recv || !r.error_string)
-    throw Fail{MRT_ERR_HIP, "RCCL (librccl.so.1) is not available; MRT_GATHER=peer uses HIP peer copies"};
+    throw Fail{MRT_ERR_HIP, "RCCL (librccl.so.1) is not available"};
   return r;
 }
 
@@ -105,6 +105,7 @@ struct DevFrame {
   uint32_t* b = nullptr;
   void* slab = nullptr;
   uint32_t count = 0;  // pixels of this device's shard
+  std::vector<uint32_t> pix;  // their indices, in slab order (host; mrt_render's per-shard upload)
   void* recv = nullptr;  // on device 0
 };
 
@@ -136,6 +137,8 @@ struct Frame {
       HIPF(hipMalloc(&f.b, npix() * 4));
       if (d.size() > 1) {
         MRTF(f.ctx, mrt_shard_pixels(W, H, shard(i), shards(), nullptr, &f.count));
+        f.pix.resize(f.count);
+        if (f.count) MRTF(f.ctx, mrt_shard_pixels(W, H, shard(i), shards(), f.pix.data(), &f.count));
         HIPF(hipMalloc(&f.slab, (size_t)f.count * 16 + 16));
       }
     }
@@ -204,8 +207,11 @@ struct Frame {
 struct MultiDev {
   std::vector<mrt_ctx*> devs;
   std::vector<int> ids;
-  bool rccl = false;
-  std::vector<ncclComm_t> comms;  // lazily, at the first RCCL gather
+  bool distinct = false;          // no device repeats (RCCL has one rank per device)
+  bool rccl = false;              // the gather uses RCCL (else peer copies)
+  int64_t mode = MRT_GATHER_AUTO;
+  std::string transport = "peer";
+  std::vector<ncclComm_t> comms;  // created with the context (distinct devices)
   Frame* scratch = nullptr;       // mrt_render's frame (host buffers)
 };
 
@@ -307,12 +313,35 @@ int multi_render(MultiDev* m, const mrt_render_args* a, float* rgb, uint32_t* bo
     if (f.d.empty() || f.W != a->width || f.H != a->height || f.si != a->shard_index || f.sc != sc)
       f.setup(m, m->devs, a->width, a->height, a->shard_index, sc);
     const size_t n = f.npix();
-    // every device starts from the caller's sums (its shard's pixels of them
-    // are what it adds to); device 0's buffer comes back whole
-    for (DevFrame& d : f.d) {
-      HIPF(hipSetDevice(d.device));
-      HIPF(hipMemcpyAsync(d.rgb, rgb, n * 12, hipMemcpyHostToDevice, d.st));
-      HIPF(hipMemcpyAsync(d.b, bounces, n * 4, hipMemcpyHostToDevice, d.st));
+    // every device starts from the caller's sums of ITS shard's pixels (what
+    // it adds to): each gets only those, packed on the host into its slab
+    // and unpacked on the device; the others' pixels arrive with the gather,
+    // so device 0's buffer comes back whole
+    {
+      std::vector<Fail> fails(f.d.size(), Fail{MRT_OK, ""});
+      std::vector<std::thread> th;
+      for (size_t i = 0; i < f.d.size(); ++i)
+        th.emplace_back([&, i] {
+          try {
+            DevFrame& d = f.d[i];
+            if (!d.count) return;
+            std::vector<uint32_t> slab((size_t)d.count * 4);
+            for (uint32_t k = 0; k < d.count; ++k) {
+              const uint32_t p = d.pix[k];
+              memcpy(&slab[4 * (size_t)k], rgb + 3 * (size_t)p, 12);
+              slab[4 * (size_t)k + 3] = bounces[p];
+            }
+            HIPF(hipSetDevice(d.device));
+            HIPF(hipMemcpyAsync(d.slab, slab.data(), slab.size() * 4, hipMemcpyHostToDevice, d.st));
+            MRTF(d.ctx, mrt_shard_unpack_device(d.ctx, f.W, f.H, f.shard(i), f.shards(), d.slab, d.rgb, d.b, d.st));
+            HIPF(hipStreamSynchronize(d.st));  // the host slab goes out of scope
+          } catch (const Fail& e) {
+            fails[i] = e;
+          }
+        });
+      for (auto& t : th) t.join();
+      for (const Fail& e : fails)
+        if (e.code != MRT_OK) throw e;
     }
     f.render(*a);
     f.gather();
@@ -330,9 +359,46 @@ int multi_render(MultiDev* m, const mrt_render_args* a, float* rgb, uint32_t* bo
   }
 }
 
+int multi_set_gather(MultiDev* m, int64_t mode, std::string& err) {
+  if (mode != MRT_GATHER_AUTO && mode != MRT_GATHER_PEER && mode != MRT_GATHER_RCCL) {
+    err = "option gather must be MRT_GATHER_AUTO, _PEER or _RCCL";
+    return MRT_ERR_INVALID;
+  }
+  if (mode == MRT_GATHER_RCCL && !m->distinct) {
+    err = "option gather: RCCL needs distinct devices (one rank per device)";
+    return MRT_ERR_INVALID;
+  }
+  if (mode != MRT_GATHER_PEER && m->distinct && m->devs.size() > 1) {
+    try {
+      ensure_comms(m);
+    } catch (const Fail& e) {
+      if (mode == MRT_GATHER_RCCL) {
+        err = e.msg;
+        return MRT_ERR_HIP;
+      }
+      m->comms.clear();
+      m->rccl = false;
+      m->mode = mode;
+      m->transport = "peer (RCCL unavailable: " + e.msg + ")";
+      err.clear();
+      return MRT_OK;
+    }
+    m->rccl = true;
+    m->transport = "rccl";
+  } else if (m->devs.size() > 1) {
+    m->rccl = false;
+    m->transport = "peer";
+  }
+  m->mode = mode;
+  err.clear();
+  return MRT_OK;
+}
+int64_t multi_gather(const MultiDev* m) { return m->mode; }
+const char* multi_transport(const MultiDev* m) { return m->transport.c_str(); }
+
 // ---- the device-resident Image ----------------------------------------------
 struct mrt_image {
-  mrt_ctx* ctx = nullptr;
+  mrt_ctx* ctx = nullptr;  // the handle it was created on (counts it: ctx_images)
   Frame f;
   uint32_t passes = 0;
   bool gathered = true;  // device 0's buffers hold every device's tiles
@@ -363,15 +429,7 @@ int mrt_create_multi(int n, const int* devices, mrt_ctx** out) {
   }
   std::vector<int> sorted = m->ids;
   std::sort(sorted.begin(), sorted.end());
-  const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-  const char* g = getenv("MRT_GATHER");
-  const std::string mode = g ? g : "";
-  if (mode == "rccl" && !distinct) {
-    multi_free(m);
-    ctx_set_error(nullptr, "MRT_GATHER=rccl needs distinct devices (RCCL has one rank per device)");
-    return MRT_ERR_INVALID;
-  }
-  m->rccl = n > 1 && distinct && mode != "peer";
+  m->distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
   // xGMI peer access from device 0 to the others and back (peer copies and
   // RCCL's P2P transport); already-enabled is fine
   for (int i = 1; i < n; ++i) {
@@ -382,8 +440,30 @@ int mrt_create_multi(int n, const int* devices, mrt_ctx** out) {
     hipDeviceEnablePeerAccess(devices[0], 0);
   }
   (void)hipGetLastError();
+  if (n == 1) {
+    m->transport = "none";
+  } else if (!m->distinct) {
+    m->transport = "peer";  // repeated devices (a rehearsal on one GPU)
+  } else {
+    // RCCL between distinct devices: opened and its communicators created
+    // now, so a missing or failing RCCL shows here and not after a render;
+    // the context then gathers with peer copies and says why
+    try {
+      ensure_comms(m);
+      m->rccl = true;
+      m->transport = "rccl";
+    } catch (const Fail& e) {
+      m->comms.clear();
+      m->transport = "peer (RCCL unavailable: " + e.msg + ")";
+    }
+  }
   *out = ctx_wrap_multi(m);
   return MRT_OK;
+}
+
+const char* mrt_context_transport(const mrt_ctx* ctx) {
+  MultiDev* m = ctx_multi(ctx);
+  return m ? m->transport.c_str() : "none";
 }
 
 int mrt_context_devices(mrt_ctx* ctx, int* n, int* devices) {
@@ -415,7 +495,10 @@ int mrt_image_create(mrt_ctx* ctx, uint32_t W, uint32_t H, mrt_image** out) {
     HIPF(hipSetDevice(img->f.d[0].device));
     HIPF(hipStreamSynchronize(img->f.d[0].st));
   });
-  if (rc == MRT_OK) *out = img.release();
+  if (rc == MRT_OK) {
+    ctx_images(ctx, +1);
+    *out = img.release();
+  }
   return rc;
 }
 
@@ -427,6 +510,7 @@ int mrt_image_destroy(mrt_image* img) {
     hipFree(img->aux);
     hipFree(img->rgb8);
   }
+  ctx_images(img->ctx, -1);
   delete img;
   return MRT_OK;
 }
@@ -469,6 +553,10 @@ int mrt_image_prepass(mrt_image* img, uint64_t seed) {
 
 int mrt_image_read(mrt_image* img, float* rgb, uint32_t* bounces, uint32_t* passes) {
   if (!img) return MRT_ERR_INVALID;
+  if (!rgb && !bounces) {  // the pass count alone: no gather, no sync
+    if (passes) *passes = img->passes;
+    return MRT_OK;
+  }
   return guard(img->ctx, [&] {
     if (!img->gathered) {
       img->f.gather();
@@ -481,6 +569,20 @@ int mrt_image_read(mrt_image* img, float* rgb, uint32_t* bounces, uint32_t* pass
     if (bounces) HIPF(hipMemcpyAsync(bounces, d0.b, n * 4, hipMemcpyDeviceToHost, d0.st));
     HIPF(hipStreamSynchronize(d0.st));
     if (passes) *passes = img->passes;
+  });
+}
+
+int mrt_image_gather(mrt_image* img) {
+  if (!img) return MRT_ERR_INVALID;
+  return guard(img->ctx, [&] {
+    if (!img->gathered) {
+      img->f.gather();
+      img->gathered = true;
+    }
+    for (DevFrame& d : img->f.d) {  // every device's queued work has ended
+      HIPF(hipSetDevice(d.device));
+      HIPF(hipStreamSynchronize(d.st));
+    }
   });
 }
 

@@ -5,10 +5,11 @@
 // (one camera path, main.rs:257-263) becomes a path slot in a pool of SoA
 // HBM buffers, advanced one segment per iteration by two kernels:
 //   k_trace : closest hit of every active ray (World::intersect)      [k2]
-//   k_shade : emit/scatter/background, path termination, regeneration of
-//             finished slots with new camera rays (Camera::ray) and wave
-//             ballot/prefix-sum compaction of the survivors           [k1,k3,k4]
-// Finished samples are written to a per-(sample,pixel) result slab and folded
+//   k_shade : emit/scatter/background, path termination and wave
+//             ballot/prefix-sum compaction of the survivors           [k3,k4]
+//   k_reserve + k_refill : new camera rays (Camera::ray) for the free
+//             slots behind the survivors                              [k1]
+// Finished samples are written to a per-(pixel,sample) result slab and folded
 // into the caller's accumulation buffers in sample order by k_accumulate [k5]
 // (Image::merge, main.rs:629-638), so the sums do not depend on scheduling
 // or on how tiles are sharded across GPUs.
@@ -234,9 +235,9 @@ __global__ __launch_bounds__(kBlock) void k_refill(DevCamera cam, RenderParams r
 // issuing for busy lanes instead of waiting for the wave's slowest ray.
 constexpr float kTmin = 0.001f;          // World::intersect(ray, 0.001, INFINITY) (main.rs trace)
 // Scheduling knobs of the persistent loop (kernel arguments so that they can
-// be tuned without a rebuild: MRT_TRACE_REFILL / _PRIM_BATCH / _CHUNK).
+// be tuned without a rebuild: options "trace_refill", "trace_chunk", ...).
 // samples per results slab at most (16 B each, one slab per queue set):
-// mrt_ctx::results_max, 2^31 = 32 GiB by default (MRT_RESULTS_LOG2 overrides)
+// mrt_ctx::results_max, 2^31 = 32 GiB by default (option "results_log2")
 constexpr uint64_t kResultsMaxLimit = 1ull << 31;
 
 struct TraceTune {
@@ -430,20 +431,19 @@ MRT_DEV bool shade_step(const DevScene& S, uint32_t max_depth, const Hit& h, V3&
   return k < max_depth;  // trace(depth 0) returns (0, 0)
 }
 
-// REGEN: finished slots take new work items from `work` here (the
-// MRT_REFILL_KERNEL=0 loop); without it (default: k_reserve + k_refill
-// generate new paths behind the survivors, and once the work counter is
-// exhausted) the regeneration code is not compiled in.
+// k_shade only shades and compacts: new camera rays go in behind the
+// survivors (k_reserve + k_refill). (Round 3's in-place regeneration of
+// finished slots is profiles/r3_experiments/ab_branches.patch.)
 // WPE: waves per SIMD the register budget is sized for (8: 64 VGPRs, 32 B of
 // scratch; 7: 71 VGPRs, none). With 8, k_shade takes more of the CU beside
 // the other queue's k_trace; a world whose records stream from the Infinity
 // Cache runs better with 7 (mesh_ply 948.6 -> 969.0, 6: 962.9 Msamples/s),
 // an L2-resident one with 8 (sphere_grid 808.8, 7: 778.1, 6: 761.0;
 // profiles/r3_tune2/wpe.txt).
-template <bool COUNT, bool EXT, bool REGEN, int WPE>
-__global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, DevCamera cam, RenderParams rp, PathBufs in,
-                                                  PathBufs out, const uint4* hits, Ctrl* ctrl, uint32_t cur,
-                                                  uint32_t* work, float4* results, DevCounters* cnt) {
+template <bool COUNT, bool EXT, int WPE>
+__global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, RenderParams rp, PathBufs in, PathBufs out,
+                                                  const uint4* hits, Ctrl* ctrl, uint32_t cur, float4* results,
+                                                  DevCounters* cnt) {
   const uint32_t n = ctrl->active[cur];
   if (blockIdx.x == 0 && threadIdx.x < kGroups) ctrl->group_next[threadIdx.x * 32] = 0;  // next k_trace
   // one workgroup per 256 live paths: the host sizes the grid from a bound on
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, DevCamera cam
     const uint32_t base = blockIdx.x * kBlock;
     if (base >= n) return;
     const uint32_t i = base + threadIdx.x;
-    bool alive = false, need = false;
+    bool alive = false;
     float4 ro{}, rd{}, thr{}, rad{};
     uint4 rs{};
     if (i < n) {
@@ -486,25 +486,11 @@ __global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, DevCamera cam
         rs = make_uint4((uint32_t)rng.s0, (uint32_t)(rng.s0 >> 32), (uint32_t)rng.s1, (uint32_t)(rng.s1 >> 32));
       } else {
         results[MRT_IDX(S, g, rp.G, 21)] = make_float4(L.x, L.y, L.z, __uint_as_float(k));
-        need = true;
         nsample += 1;
       }
     }
-    // regenerate finished slots from the work counter and compact survivors
-    // into the next pool: one atomic per workgroup for each (same-address
-    // atomics from every wave serialise in L2)
-    // (REGEN only; otherwise no reservation, barrier round or device atomic)
-    const unsigned long long need_mask = __ballot(need);
-    const uint32_t wbase = REGEN ? wg_reserve(work, (uint32_t)__popcll(need_mask), wave, s_cnt, s_base) : rp.G;
-    if (REGEN && need) {
-      uint32_t g = wbase + lane_rank(need_mask);
-      if (g < rp.G) {
-        gen_work(cam, rp, g, ro, rd, rs);
-        thr = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-        alive = true;
-      }
-    }
-    // compact survivors + new paths into the next pool
+    // compact the survivors into the next pool: one atomic per workgroup
+    // (same-address atomics from every wave serialise in L2)
     const unsigned long long alive_mask = __ballot(alive);
     const uint32_t obase = wg_reserve(&ctrl->active[cur ^ 1], (uint32_t)__popcll(alive_mask), wave, s_cnt, s_base);
     if (alive) {
@@ -520,7 +506,7 @@ __global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, DevCamera cam
 }
 
 // The whole path loop in one persistent kernel: every lane owns a path
-// (work item g = sample*n_pix + pixel), steps its closest-hit traversal like
+// (work item g = pixel*spp + sample, gen_work), steps its closest-hit traversal like
 // k_trace, and when a segment ends shades it in place (shade_step) and
 // continues with the scattered ray — no pool buffers, no per-bounce launch
 // and no per-launch tail. Finished paths write results[g] (accumulated in
@@ -938,15 +924,63 @@ __global__ __launch_bounds__(kBlock) void k_selftest_slab(unsigned long long n, 
 // last long rays on few lanes) overlaps the other queues' kernels instead of
 // idling the GPU.
 constexpr int kMaxQueues = 4;
+
+// Context options (mrt_set_option / mrt_get_option, massrt.h): the tuning
+// knobs of the loop, set by the caller per context — never read from the
+// process environment. -1 (where allowed) = the per-scene rule chosen at
+// upload (apply_options). Measurements behind each default: DESIGN.md §4.
+enum OptId {
+  OPT_QUEUES,            // path pools on their own streams (2: one's tail overlaps the other's kernels)
+  OPT_POOL_PATHS,        // live paths at most over all queues (384M: 66 GiB)
+  OPT_RESULTS_LOG2,      // samples per results slab at most, log2 (31: a 1080p x 1024-spp frame in one chunk)
+  OPT_FINISH_PATHS,      // drain hand-off threshold (fused adopt-mode launch); 0 = never
+  OPT_FINISH_GRID_DIV,   // the hand-off launch takes 1/div of its occupancy grid
+  OPT_TRACE_REFILL,      // k_trace: refill a wave once this many lanes are idle (-1: 32)
+  OPT_TRACE_BOX_MIN,     // k_trace: box run while this many lanes are at a box (-1: 16 instanced / 32 big / 24)
+  OPT_TRACE_CHUNK,       // k_trace: rays per work grab (-1: 128 big or instanced / 512)
+  OPT_TRACE_PRIM_BATCH,  // k_trace: primitive step once this many lanes wait at one
+  OPT_TRACE_WGS_PER_CU,  // persistent grids: workgroups per CU (0: occupancy, 3/4 of it beside other queues)
+  OPT_SHADE_WAVES,       // k_shade register budget, waves per SIMD: 7 or 8 (-1: 7 for big non-instanced worlds)
+  OPT_SHADE_BATCH,       // k_render: shade once this many lanes finished a segment
+  OPT_TREELET_KB,        // LDS treelet per workgroup, KiB (0: none); applies at the next upload
+  OPT_TRACE_BLOCK,       // k_trace workgroup size beside a treelet: 256, 512 or 1024
+  OPT_MEM_RESERVE_MB,    // device memory a render leaves free when it sizes the pool and results slab
+  kNumOpts
+};
+struct OptDef {
+  const char* name;
+  int64_t def, lo, hi;
+};
+constexpr OptDef kOptDefs[kNumOpts] = {
+    {"queues", 2, 1, kMaxQueues},
+    {"pool_paths", (int64_t)384 << 20, 1 << 16, 1 << 30},
+    {"results_log2", 31, 10, 31},
+    {"finish_paths", 500000, 0, 1 << 30},
+    {"finish_grid_div", 1, 1, 64},
+    {"trace_refill", -1, -1, 64},
+    {"trace_box_min", -1, -1, 65},
+    {"trace_chunk", -1, -1, 1 << 20},
+    {"trace_prim_batch", 1, 1, 64},
+    {"trace_wgs_per_cu", 0, 0, 32},
+    {"shade_waves", -1, -1, 8},
+    {"shade_batch", 16, 1, 64},
+    {"treelet_kb", 0, 0, 150},
+    {"trace_block", 256, 256, 1024},
+    {"mem_reserve_mb", 4096, 0, 1 << 20},
+};
+int opt_find(const char* name) {
+  if (!name) return -1;
+  for (int i = 0; i < kNumOpts; ++i)
+    if (!strcmp(kOptDefs[i].name, name)) return i;
+  return -1;
+}
 struct Queue {
   hipStream_t stream = nullptr;
   PathBufs bufs[2]{};
   uint4* hits = nullptr;
   size_t cap = 0;
   Ctrl* ctrl = nullptr;        // device
-  Ctrl* h_status = nullptr;    // pinned, 2 slots (lagged status reads)
-  uint32_t* h_work = nullptr;  // pinned, 2 slots: snapshots of the shared work counter
-  HostStatus* h_stat = nullptr;  // pinned coherent, 2 slots, written by k_status
+  HostStatus* h_stat = nullptr;  // pinned coherent, 2 slots, written by k_status (lagged status reads)
   HostStatus* d_stat = nullptr;  // the same memory as the device addresses it
   hipEvent_t ev[2]{};
   hipEvent_t join = nullptr;
@@ -955,6 +989,7 @@ struct Queue {
 struct mrt_ctx {
   int device = 0;
   MultiDev* multi = nullptr;  // a context over several devices (frames.hip): the rest is unused
+  int images = 0;             // live mrt_image objects created on this handle
   hipStream_t stream = nullptr;
   std::string err;
   // scene
@@ -968,23 +1003,22 @@ struct mrt_ctx {
   size_t pool_cap = 0;  // paths over all queues
   void* pool_mem = nullptr;
   Queue q[kMaxQueues];
-  int n_queues = 2;            // MRT_QUEUES overrides (1..4)
+  int64_t opt[kNumOpts];       // mrt_set_option values (kOptDefs); derived fields below (apply_options)
+  bool scene_big = false;      // the record stream is past half the chip's L2 (per-scene rules)
+  uint32_t scene_instances = 0;
+  int n_queues = 2;            // option "queues"
   uint32_t* work = nullptr;    // shared work counter of the wavefront loop (word 1: tonemap max count)
   uint32_t* gamma_d = nullptr; // display: gamma byte thresholds (256 words)
   hipEvent_t fork = nullptr;
-  float4* results = nullptr;
+  float4* results = nullptr;  // the results slab (results_cap samples)
   size_t results_cap = 0;
-  // Queue sets (round 2): consecutive render chunks alternate between two
-  // sets of n_queues queues, each with its own work counter (word 32*s of
-  // `work`) and results slab (results_s[s]); a chunk returns to the caller as
-  // soon as every queue of its set has handed its drain to a finish launch,
-  // so the next chunk's paths start while those drains run. acc_done[s]:
-  // recorded on the caller's stream after the accumulate that read slab s.
-  int n_sets = 1;  // MRT_QUEUE_SETS=2: two sets (when 2 * n_queues <= kMaxQueues)
-  int set_next = 0;
-  float4* results_s[2] = {nullptr, nullptr};
-  hipEvent_t acc_done[2] = {nullptr, nullptr};
-  hipEvent_t set_fork[2] = {nullptr, nullptr};
+  // acc_done: recorded on the caller's stream after the accumulate that read
+  // the results slab (and after any other caller-stream work on the shared
+  // buffers, mark_ctx_busy); the next render's queues fork after it.
+  // (Round 2's two alternating queue sets, measured 5-12% slower, are in
+  // profiles/r3_experiments/ab_branches.patch.)
+  hipEvent_t acc_done = nullptr;
+  hipEvent_t set_fork = nullptr;
   // kernel-timing marks resolved lazily (mrt_get_kernel_stats): a timed
   // render does not wait for its set's drain
   std::vector<std::array<hipEvent_t, 3>> pend_marks;
@@ -1012,31 +1046,24 @@ struct mrt_ctx {
   size_t pool_paths = (size_t)384 << 20;
   int cus = 1;
   bool trace_lds = false;          // the scene has an LDS treelet (set per scene)
-  bool tune_auto_loop = true;      // refill/box_min chosen per scene (unless MRT_TRACE_REFILL/BOX_MIN set)
-  bool tune_auto_chunk = true;     // rays per grab chosen per scene (unless MRT_TRACE_CHUNK set)
-  int shade_wpe = 8;               // k_shade register budget: 8 or 7 waves/SIMD (per scene; MRT_SHADE_WPE)
-  bool shade_wpe_auto = true;
+  int shade_wpe = 8;               // k_shade register budget: 8 or 7 waves/SIMD (option "shade_waves")
   uint32_t tl_boxes = 0;           // box records in the treelet
   // LDS treelet: off by default. Measured: it removes the
   // global load of a step only when every lane of the wave is in the copy,
   // and the TA cost is per wave instruction, not per lane — 256/16 KB and
   // 1024/78 KB were 1% and 1-4% slower than no treelet.
-  int trace_block = 256;           // k_trace workgroup size with a treelet (MRT_TRACE_BLOCK: 256, 512 or 1024)
-  uint32_t treelet_kb = 0;         // treelet budget per workgroup (MRT_TREELET_KB; 0 = none)
+  int trace_block = 256;           // k_trace workgroup size with a treelet (option "trace_block")
+  uint32_t treelet_kb = 0;         // treelet budget per workgroup (option "treelet_kb"; 0 = none)
   // a queue whose work is exhausted hands its last <= finish_paths paths to
   // one fused k_render launch (adopt mode) instead of per-bounce launches
   // (MRT_FINISH_PATHS; 0 = never). 500k measured best (profiles/r2_experiments/
   // finish_sweep.txt): mesh_ply 545 -> 678, sphere_grid 638 -> 642 Msamples/s
   uint32_t finish_paths = 500000;
-  // new camera rays: generated by k_reserve + k_refill behind the compacted
-  // survivors (true), or by k_shade into each finished slot (MRT_REFILL_KERNEL=0)
-  bool refill_kernel = true;
-  // lagged status reads by k_status into pinned coherent memory (true), or by
-  // hipMemcpyAsync (MRT_STATUS_KERNEL=0)
-  bool status_kernel = true;
   uint32_t refill_grid = 2048;  // k_refill workgroups (grid-stride; cus * 8)
-  uint64_t results_max = kResultsMaxLimit;  // samples per results slab (MRT_RESULTS_LOG2: 10..31)
-  uint32_t finish_grid_div = 1;  // the finish launch takes 1/div of its occupancy grid (MRT_FINISH_GRID_DIV)
+  uint64_t results_max = kResultsMaxLimit;  // samples per results slab (option "results_log2")
+  uint32_t finish_grid_div = 1;  // the finish launch takes 1/div of its occupancy grid (option "finish_grid_div")
+  uint32_t wgs_per_cu = 0;       // option "trace_wgs_per_cu" (0: occupancy)
+  size_t mem_reserve = (size_t)4096 << 20;  // option "mem_reserve_mb"
 
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t*, uint32_t>> pixlists;
   // host-buffer render staging
@@ -1064,6 +1091,9 @@ mrt_ctx* ctx_wrap_multi(MultiDev* m) {
   return c;
 }
 MultiDev* ctx_multi(const mrt_ctx* c) { return c ? c->multi : nullptr; }
+void ctx_images(mrt_ctx* c, int delta) {
+  if (c) c->images += delta;
+}
 void ctx_set_error(mrt_ctx* c, const std::string& msg) {
   if (c)
     c->err = msg;
@@ -1103,6 +1133,64 @@ int on_each(mrt_ctx* c, F&& f) {
 namespace {
 
 void set_device(mrt_ctx* c) { HIP_CHECK(hipSetDevice(c->device)); }
+
+// Derived fields from the options; options left at -1 take the per-scene
+// rules (scene_big / scene_instances, set at upload):
+//  * box run / refill (profiles/r2_tune, r3_tune.txt): refill 32
+//    everywhere; box run while >= 16 lanes are at a box for an
+//    instance-heavy world (cube_field 266 -> 275, Menger 37.3 -> 44.1
+//    Msamples/s), >= 32 for another stream past half the chip's L2 (its
+//    record round trips go to the Infinity Cache; mesh_ply 749 -> 775), else
+//    >= 24 (sphere_grid);
+//  * rays per grab (profiles/r3_tune2/): an L2-resident world without many
+//    instances runs longer stretches of neighbouring rays per wave
+//    (sphere_grid 762.8 / 775.0 / 780.3 / 780.6 at 128 / 256 / 512 / 1024),
+//    while big or instanced worlds keep 128 (mesh_ply 897.4 -> 841.4 at 1024:
+//    its waves end on longer tails);
+//  * k_shade at 7 waves/SIMD for a big non-instanced world (mesh_ply 948.6
+//    -> 969.0), else 8 (sphere_grid 808.8, 7: 778.1; profiles/r3_tune2/wpe.txt).
+void apply_options(mrt_ctx* c) {
+  const int64_t* o = c->opt;
+  const bool inst = c->scene_instances > 1000, big = c->scene_big;
+  c->n_queues = (int)o[OPT_QUEUES];
+  c->pool_paths = (size_t)o[OPT_POOL_PATHS];
+  c->results_max = 1ull << o[OPT_RESULTS_LOG2];
+  c->finish_paths = (uint32_t)o[OPT_FINISH_PATHS];
+  c->finish_grid_div = (uint32_t)o[OPT_FINISH_GRID_DIV];
+  c->tune.refill = o[OPT_TRACE_REFILL] >= 0 ? (uint32_t)std::max<int64_t>(1, o[OPT_TRACE_REFILL]) : 32u;
+  c->tune.box_min = o[OPT_TRACE_BOX_MIN] >= 0 ? (uint32_t)std::max<int64_t>(1, o[OPT_TRACE_BOX_MIN])
+                                              : (inst ? 16u : (big ? 32u : 24u));
+  c->tune.chunk = o[OPT_TRACE_CHUNK] >= 0 ? (uint32_t)o[OPT_TRACE_CHUNK] : ((big || inst) ? 128u : 512u);
+  c->tune.prim_batch = (uint32_t)o[OPT_TRACE_PRIM_BATCH];
+  c->tune.shade_batch = (uint32_t)o[OPT_SHADE_BATCH];
+  c->shade_wpe = o[OPT_SHADE_WAVES] >= 0 ? (int)o[OPT_SHADE_WAVES] : ((big && !inst) ? 7 : 8);
+  c->treelet_kb = (uint32_t)o[OPT_TREELET_KB];
+  c->trace_block = (int)o[OPT_TRACE_BLOCK];
+  c->mem_reserve = (size_t)o[OPT_MEM_RESERVE_MB] << 20;
+  if (c->wgs_per_cu != (uint32_t)o[OPT_TRACE_WGS_PER_CU]) c->grids.clear();
+  c->wgs_per_cu = (uint32_t)o[OPT_TRACE_WGS_PER_CU];
+}
+
+// Validates and stores option `id`; the caller re-derives (apply_options).
+void set_option(mrt_ctx* c, int id, int64_t v) {
+  const OptDef& d = kOptDefs[id];
+  if (v < d.lo || v > d.hi)
+    throw ApiError{MRT_ERR_INVALID, std::string("option ") + d.name + " out of range [" + std::to_string(d.lo) + ", " +
+                                        std::to_string(d.hi) + "]"};
+  if (id == OPT_TRACE_BLOCK && v != 256 && v != 512 && v != 1024)
+    throw ApiError{MRT_ERR_INVALID, "option trace_block must be 256, 512 or 1024"};
+  if (id == OPT_SHADE_WAVES && v != -1 && v != 7 && v != 8)
+    throw ApiError{MRT_ERR_INVALID, "option shade_waves must be 7, 8 or -1 (per scene)"};
+  if (id == OPT_TRACE_CHUNK && v != -1 && v < 64) throw ApiError{MRT_ERR_INVALID, "option trace_chunk must be >= 64 or -1"};
+  if (id == OPT_QUEUES && v != c->opt[id] && c->pool_mem) {  // the pool is split per queue: reallocated at the next render
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipFree(c->pool_mem));
+    c->pool_mem = nullptr;
+    c->pool_cap = 0;
+    c->grids.clear();  // k_trace's grid share depends on the queue count
+  }
+  c->opt[id] = v;
+}
 
 template <typename F>
 int guarded(mrt_ctx* c, F&& f) {
@@ -1158,7 +1246,7 @@ uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem, bool shared = f
   int per_cu = 0;
   HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, smem));
   if (shared) per_cu = std::max(1, per_cu * 3 / 4);
-  if (const char* e = getenv("MRT_TRACE_WGS_PER_CU")) per_cu = atoi(e);
+  if (c->wgs_per_cu) per_cu = (int)c->wgs_per_cu;
   const uint32_t g = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
   c->grids[key] = g;
   return g;
@@ -1233,24 +1321,31 @@ uint32_t shade_grid(const Queue& q, size_t bound) {
   return (uint32_t)std::max<size_t>(1, (n + kBlock - 1) / kBlock);
 }
 
-// P paths per queue set (n_queues queues), allocated for every set.
+// device bytes of a pool of P paths over the context's queues: two state
+// sets (5 x 16 B each) + the hit record per path, 256-B aligned sections
+constexpr size_t kPathBytes = 16 * (2 * 5 + 1);
+size_t pool_bytes(const mrt_ctx* c, size_t P) {
+  const size_t K = (size_t)c->n_queues, per_q = (P + K - 1) / K;
+  return (kPathBytes * per_q + 4096) * K;
+}
+
+// P paths over the context's queues.
 void ensure_pool(mrt_ctx* c, size_t P) {
   if (P <= c->pool_cap) return;
-  HIP_CHECK(hipDeviceSynchronize());  // a set may still be draining into the old pool
+  HIP_CHECK(hipDeviceSynchronize());  // the queues may still be draining into the old pool
   if (c->pool_mem) HIP_CHECK(hipFree(c->pool_mem));
   c->pool_mem = nullptr;
   c->pool_cap = 0;
   const int K = c->n_queues;
   const size_t per_q = (P + K - 1) / K;
-  const size_t per = 16 * (2 * 5 + 1);  // two state sets + hits
-  HIP_CHECK(hipMalloc(&c->pool_mem, (per * per_q + 4096) * K * c->n_sets));
+  HIP_CHECK(hipMalloc(&c->pool_mem, pool_bytes(c, P)));
   char* p = (char*)c->pool_mem;
   auto take = [&](size_t bytes) {
     char* r = p;
     p += (bytes + 255) & ~(size_t)255;
     return r;
   };
-  for (int k = 0; k < K * c->n_sets; ++k) {
+  for (int k = 0; k < K; ++k) {
     Queue& q = c->q[k];
     for (int b = 0; b < 2; ++b) {
       q.bufs[b].ro = (float4*)take(16 * per_q);
@@ -1265,17 +1360,57 @@ void ensure_pool(mrt_ctx* c, size_t P) {
   c->pool_cap = per_q * K;
 }
 
-// n samples per results slab, one slab per queue set (results == results_s[0]).
+// n samples in the results slab.
 void ensure_results(mrt_ctx* c, size_t n) {
   if (n <= c->results_cap) return;
-  HIP_CHECK(hipDeviceSynchronize());  // a set may still write or accumulate the old slabs
-  for (int s = 0; s < 2; ++s) {
-    if (c->results_s[s]) HIP_CHECK(hipFree(c->results_s[s]));
-    c->results_s[s] = nullptr;
-  }
-  for (int s = 0; s < c->n_sets; ++s) HIP_CHECK(hipMalloc(&c->results_s[s], 16 * n));
-  c->results = c->results_s[0];
+  HIP_CHECK(hipDeviceSynchronize());  // the queues may still write or accumulate the old slab
+  if (c->results) HIP_CHECK(hipFree(c->results));
+  c->results = nullptr;
+  c->results_cap = 0;
+  HIP_CHECK(hipMalloc(&c->results, 16 * n));
   c->results_cap = n;
+}
+
+// Sizes a render's path pool and results slab to the device:
+// they must fit the memory free now minus mem_reserve, since several
+// contexts may share one device (a multi-device context over {0,0,0}, ranks
+// rehearsed on one GPU) and the defaults alone ask for ~98 GiB. When either
+// buffer has to grow both are released and planned afresh: the pool shrinks
+// first (its size barely matters from 128M paths on), down to
+// kPoolFloor paths, then the samples per results chunk (more chunks, the
+// same image: chunks accumulate in sample order). The planning of the
+// contexts of a process is serialised, so each sees the others' buffers.
+constexpr size_t kPoolFloor = (size_t)64 << 20;
+std::mutex g_alloc_mutex;
+void plan_buffers(mrt_ctx* c, uint32_t n_pix, uint32_t& spp_chunk, bool need_pool) {
+  std::lock_guard<std::mutex> lock(g_alloc_mutex);
+  size_t P = need_pool ? std::min<size_t>((size_t)n_pix * spp_chunk, c->pool_paths) : 0;
+  if (P <= c->pool_cap && (size_t)n_pix * spp_chunk <= c->results_cap) return;
+  HIP_CHECK(hipDeviceSynchronize());  // the queues may still use the old buffers
+  if (c->pool_mem) HIP_CHECK(hipFree(c->pool_mem));
+  c->pool_mem = nullptr;
+  c->pool_cap = 0;
+  if (c->results) HIP_CHECK(hipFree(c->results));
+  c->results = nullptr;
+  c->results_cap = 0;
+  size_t free_b = 0, total_b = 0;
+  HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+  const size_t budget = free_b > c->mem_reserve ? free_b - c->mem_reserve : 0;
+  for (;;) {
+    const size_t need = (P ? pool_bytes(c, P) : 0) + (size_t)n_pix * spp_chunk * 16;
+    if (need <= budget) break;
+    if (P > kPoolFloor) {
+      P = std::max(kPoolFloor, P / 2);
+    } else if (spp_chunk > 1) {
+      spp_chunk = spp_chunk / 2;
+      if (P) P = std::min<size_t>(P, (size_t)n_pix * spp_chunk);
+    } else {
+      throw ApiError{MRT_ERR_NOMEM, "device memory: " + std::to_string(free_b >> 20) + " MiB free, mem_reserve_mb " +
+                                        std::to_string(c->mem_reserve >> 20) + ": not even one sample per pixel fits"};
+    }
+  }
+  if (P) ensure_pool(c, P);
+  ensure_results(c, (size_t)n_pix * spp_chunk);
 }
 
 void ensure_slots(mrt_ctx* c, size_t n) {
@@ -1360,18 +1495,16 @@ void launch_finish_v(mrt_ctx* c, int qi, uint32_t cur, const RenderParams& rp, b
 
 // Work enqueued on a caller's stream `st` that writes the context's shared
 // buffers (q[0].ctrl, the results slab, the lane-ray slots): the next
-// wavefront render forks its queues after acc_done[s], so recording every
-// set's acc_done here orders that render after this work too.
-void mark_ctx_busy(mrt_ctx* c, hipStream_t st) {
-  for (int s = 0; s < c->n_sets; ++s) HIP_CHECK(hipEventRecord(c->acc_done[s], st));
-}
+// wavefront render forks its queues after acc_done, so recording it here
+// orders that render after this work too.
+void mark_ctx_busy(mrt_ctx* c, hipStream_t st) { HIP_CHECK(hipEventRecord(c->acc_done, st)); }
 
 // The fused path loop: one k_render launch + one k_accumulate per chunk.
 void render_fused(mrt_ctx* c, const mrt_render_args* a, const uint32_t* pixlist_d, uint32_t n_pix, uint32_t spp_chunk,
                   float* d_rgb, uint32_t* d_b, hipStream_t st) {
   const bool count = (a->flags & MRT_RENDER_COUNTERS) != 0;
   const bool timing = (a->flags & MRT_RENDER_TIME_KERNELS) != 0;
-  ensure_results(c, (size_t)n_pix * spp_chunk);
+  plan_buffers(c, n_pix, spp_chunk, false);
   wait_queues(c, st);
   for (uint32_t done = 0; done < a->spp_count; done += spp_chunk) {
     const uint32_t cs = std::min(spp_chunk, a->spp_count - done);
@@ -1441,9 +1574,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
     render_fused(c, a, pl.first, n_pix, spp_chunk, d_rgb, d_b, st);
     return;
   }
-  const size_t pool = std::min<size_t>((size_t)n_pix * spp_chunk, c->pool_paths);
-  ensure_pool(c, pool);
-  ensure_results(c, (size_t)n_pix * spp_chunk);
+  plan_buffers(c, n_pix, spp_chunk, true);
   const int K = c->n_queues;
   const bool timing = (a->flags & MRT_RENDER_TIME_KERNELS) != 0;
   if (timing && c->pend_marks.size() + c->pend_fin.size() > kMaxPendingMarks) resolve_kernel_timing(c);
@@ -1482,25 +1613,21 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
       // trace(ray, 0) returns (0, 0) for every sample: nothing to add
       continue;
     }
-    // queue set s: its queues, work counter and results slab
-    const int s = c->set_next;
-    c->set_next = (c->set_next + 1) % c->n_sets;
-    const int qb = s * K;
-    uint32_t* work = c->work + 32 * s;
-    float4* res = c->results_s[s];
-    // fork: set s starts after the accumulate that last read slab s
-    // (acc_done[s], on the caller's stream) — not after everything on `st`,
-    // which may hold the other set's accumulate still waiting for its drain
-    // (the kernels read nothing else the caller's stream writes)
+    // the queues, their shared work counter and the results slab
+    uint32_t* work = c->work;
+    float4* res = c->results;
+    // fork: the queues start after the accumulate that last read the slab
+    // (acc_done, on the caller's stream; the kernels read nothing else the
+    // caller's stream writes)
     const uint32_t n0 = (uint32_t)std::min<size_t>(rp.G, c->pool_cap);
-    HIP_CHECK(hipStreamWaitEvent(c->q[qb].stream, c->acc_done[s], 0));
-    HIP_CHECK(hipMemcpyAsync(work, &n0, 4, hipMemcpyHostToDevice, c->q[qb].stream));
-    HIP_CHECK(hipEventRecord(c->set_fork[s], c->q[qb].stream));
+    HIP_CHECK(hipStreamWaitEvent(c->q[0].stream, c->acc_done, 0));
+    HIP_CHECK(hipMemcpyAsync(work, &n0, 4, hipMemcpyHostToDevice, c->q[0].stream));
+    HIP_CHECK(hipEventRecord(c->set_fork, c->q[0].stream));
     uint32_t base = 0;
     for (int k = 0; k < K; ++k) {
-      Queue& q = c->q[qb + k];
+      Queue& q = c->q[k];
       const uint32_t nk = (uint32_t)(((uint64_t)n0 * (k + 1)) / K) - base;  // <= q.cap
-      if (k) HIP_CHECK(hipStreamWaitEvent(q.stream, c->set_fork[s], 0));
+      if (k) HIP_CHECK(hipStreamWaitEvent(q.stream, c->set_fork, 0));
       Ctrl init{{nk, 0}, 0, 0};
       HIP_CHECK(hipMemcpyAsync(q.ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice, q.stream));
       if (nk) {
@@ -1518,12 +1645,24 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
       int slot = 0;
       bool pending = false, finished = false;
       size_t bound = ~(size_t)0;  // live paths at most (shade_grid)
-      bool exhausted = false;     // the work counter was seen at or past G: k_shade need not regenerate
+      bool exhausted = false;     // the work counter was seen at or past G: no refill
     } st_[kMaxQueues];
     int open = K;
+    // an internal error in the middle of a chunk: every queue's kernels end
+    // before the error returns, so the next render does not fork onto pools
+    // and a results slab that this chunk's launches still write
+    auto fail_chunk = [&](const std::string& msg) {
+      for (int k = 0; k < K; ++k) (void)hipStreamSynchronize(c->q[k].stream);
+      throw ApiError{MRT_ERR_HIP, msg};
+    };
+    auto* shade = c->shade_wpe == 7
+                      ? (count ? (c->scene_ext ? k_shade<true, true, 7> : k_shade<true, false, 7>)
+                               : (c->scene_ext ? k_shade<false, true, 7> : k_shade<false, false, 7>))
+                      : (count ? (c->scene_ext ? k_shade<true, true, 8> : k_shade<true, false, 8>)
+                               : (c->scene_ext ? k_shade<false, true, 8> : k_shade<false, false, 8>));
     while (open > 0) {
       for (int k = 0; k < K; ++k) {
-        Queue& q = c->q[qb + k];
+        Queue& q = c->q[k];
         Loop& L = st_[k];
         if (L.finished) continue;
         for (int b = 0; b < kBatch; ++b, ++L.it) {
@@ -1547,21 +1686,10 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
             m[1] = next_event();
             HIP_CHECK(hipEventRecord(m[1], q.stream));
           }
-          {
-            const bool regen = !(L.exhausted || c->refill_kernel);
-            auto* shade =
-                regen ? (count ? (c->scene_ext ? k_shade<true, true, true, 8> : k_shade<true, false, true, 8>)
-                               : (c->scene_ext ? k_shade<false, true, true, 8> : k_shade<false, false, true, 8>))
-                : c->shade_wpe == 7
-                    ? (count ? (c->scene_ext ? k_shade<true, true, false, 7> : k_shade<true, false, false, 7>)
-                             : (c->scene_ext ? k_shade<false, true, false, 7> : k_shade<false, false, false, 7>))
-                    : (count ? (c->scene_ext ? k_shade<true, true, false, 8> : k_shade<true, false, false, 8>)
-                             : (c->scene_ext ? k_shade<false, true, false, 8> : k_shade<false, false, false, 8>));
-            hipLaunchKernelGGL(shade, dim3(shade_grid(q, L.bound)), dim3(kBlock), 0, q.stream, c->S, c->cam, rp, q.bufs[cur],
-                               q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, work, res, c->d_cnt);
-          }
+          hipLaunchKernelGGL(shade, dim3(shade_grid(q, L.bound)), dim3(kBlock), 0, q.stream, c->S, rp, q.bufs[cur],
+                             q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, res, c->d_cnt);
           HIP_CHECK(hipGetLastError());
-          if (c->refill_kernel && !L.exhausted) {  // new paths behind the survivors
+          if (!L.exhausted) {  // new paths behind the survivors
             hipLaunchKernelGGL(k_reserve, dim3(1), dim3(64), 0, q.stream, q.ctrl, cur, work, rp.G, rp.pool_cap);
             hipLaunchKernelGGL(k_refill, dim3(c->refill_grid), dim3(kBlock), 0, q.stream, c->cam, rp, q.bufs[cur ^ 1],
                                (const Ctrl*)q.ctrl);
@@ -1573,28 +1701,17 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
             marks.push_back(m);
           }
         }
-        if (c->status_kernel) {
-          hipLaunchKernelGGL(k_status, dim3(1), dim3(64), 0, q.stream, (const Ctrl*)q.ctrl, (const uint32_t*)work,
-                             q.d_stat + L.slot);
-          HIP_CHECK(hipGetLastError());
-        } else {
-          HIP_CHECK(hipMemcpyAsync(&q.h_status[L.slot], q.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, q.stream));
-          HIP_CHECK(hipMemcpyAsync(&q.h_work[L.slot], work, 4, hipMemcpyDeviceToHost, q.stream));
-        }
+        hipLaunchKernelGGL(k_status, dim3(1), dim3(64), 0, q.stream, (const Ctrl*)q.ctrl, (const uint32_t*)work,
+                           q.d_stat + L.slot);
+        HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipEventRecord(q.ev[L.slot], q.stream));
         if (L.pending) {  // the previous batch's status (one batch stays in flight)
           HIP_CHECK(hipEventSynchronize(q.ev[L.slot ^ 1]));
-          HostStatus s;
-          if (c->status_kernel) {
-            const volatile HostStatus& v = q.h_stat[L.slot ^ 1];  // written by the GPU
-            s = HostStatus{v.active0, v.active1, v.shade_short, v.work};
-          } else {
-            const Ctrl& h = q.h_status[L.slot ^ 1];
-            s = HostStatus{h.active[0], h.active[1], h.shade_short, q.h_work[L.slot ^ 1]};
-          }
+          const volatile HostStatus& v = q.h_stat[L.slot ^ 1];  // written by the GPU
+          const HostStatus s{v.active0, v.active1, v.shade_short, v.work};
           if (s.shade_short)
-            throw ApiError{MRT_ERR_HIP, "internal: a k_shade grid was smaller than its live pool (" +
-                                            std::to_string(s.shade_short) + " paths)"};
+            fail_chunk("internal: a k_shade grid was smaller than its live pool (" + std::to_string(s.shade_short) +
+                       " paths)");
           if (s.work >= rp.G) {
             L.bound = std::min<size_t>(L.bound, s.active0);
             L.exhausted = true;
@@ -1609,9 +1726,9 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
                 HIP_CHECK(hipEventRecord(fm[0], q.stream));
               }
               if (c->scene_alpha)
-                launch_finish_v<true>(c, qb + k, L.it & 1, rp, count, res);
+                launch_finish_v<true>(c, k, L.it & 1, rp, count, res);
               else
-                launch_finish_v<false>(c, qb + k, L.it & 1, rp, count, res);
+                launch_finish_v<false>(c, k, L.it & 1, rp, count, res);
               if (timing) {
                 fm[1] = next_event();
                 HIP_CHECK(hipEventRecord(fm[1], q.stream));
@@ -1624,15 +1741,14 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
         }
         L.pending = true;
         L.slot ^= 1;
-        if (L.it > 64u * 1024u) throw ApiError{MRT_ERR_HIP, "render did not converge"};
+        if (L.it > 64u * 1024u) fail_chunk("render did not converge");
       }
     }
-    // join: `st` continues after every queue of the set (which may still be
-    // running its drain: the host does not wait, the next chunk takes the
-    // other set)
+    // join: `st` continues after every queue (which may still be running its
+    // drain: the host does not wait)
     for (int k = 0; k < K; ++k) {
-      HIP_CHECK(hipEventRecord(c->q[qb + k].join, c->q[qb + k].stream));
-      HIP_CHECK(hipStreamWaitEvent(st, c->q[qb + k].join, 0));
+      HIP_CHECK(hipEventRecord(c->q[k].join, c->q[k].stream));
+      HIP_CHECK(hipStreamWaitEvent(st, c->q[k].join, 0));
     }
     if (timing) {  // resolved by mrt_get_kernel_stats (resolve_kernel_timing)
       c->pend_marks.insert(c->pend_marks.end(), marks.begin(), marks.end());
@@ -1641,7 +1757,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
     hipLaunchKernelGGL(k_accumulate, dim3((n_pix + kBlock - 1) / kBlock), dim3(kBlock), 0, st, (const float4*)res,
                        n_pix, cs, (const uint32_t*)pl.first, d_rgb, d_b);
     HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipEventRecord(c->acc_done[s], st));  // slab s is free again after this
+    HIP_CHECK(hipEventRecord(c->acc_done, st));  // the slab is free again after this
   }
 }
 
@@ -1699,13 +1815,12 @@ int mrt_create(int device, mrt_ctx** out) {
   c->device = device;
   int rc = guarded(c, [&] {
     HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    if (const char* e = getenv("MRT_QUEUES")) c->n_queues = std::max(1, std::min(kMaxQueues, atoi(e)));
+    for (int i = 0; i < kNumOpts; ++i) c->opt[i] = kOptDefs[i].def;
+    apply_options(c);
     for (int k = 0; k < kMaxQueues; ++k) {
       Queue& q = c->q[k];
       HIP_CHECK(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
       HIP_CHECK(hipMalloc(&q.ctrl, sizeof(Ctrl)));
-      HIP_CHECK(hipHostMalloc(&q.h_status, 2 * sizeof(Ctrl), hipHostMallocDefault));
-      HIP_CHECK(hipHostMalloc(&q.h_work, 2 * sizeof(uint32_t), hipHostMallocDefault));
       HIP_CHECK(hipHostMalloc(&q.h_stat, 2 * sizeof(HostStatus), hipHostMallocCoherent | hipHostMallocMapped));
       memset(q.h_stat, 0, 2 * sizeof(HostStatus));
       HIP_CHECK(hipHostGetDevicePointer((void**)&q.d_stat, q.h_stat, 0));
@@ -1716,15 +1831,8 @@ int mrt_create(int device, mrt_ctx** out) {
     HIP_CHECK(hipMalloc(&c->work, 256));
     HIP_CHECK(hipMemset(c->work, 0, 256));
     HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
-    // one queue set unless MRT_QUEUE_SETS=2 (and both sets fit in kMaxQueues):
-    // two sets let a chunk's drain overlap the next chunk, but measured 5-12%
-    // slower (profiles/r2_experiments/queue_sets.txt)
-    if (const char* e = getenv("MRT_QUEUE_SETS"))
-      c->n_sets = (atoi(e) >= 2 && 2 * c->n_queues <= kMaxQueues) ? 2 : 1;
-    for (int s = 0; s < 2; ++s) {
-      HIP_CHECK(hipEventCreateWithFlags(&c->acc_done[s], hipEventDisableTiming));
-      HIP_CHECK(hipEventCreateWithFlags(&c->set_fork[s], hipEventDisableTiming));
-    }
+    HIP_CHECK(hipEventCreateWithFlags(&c->acc_done, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&c->set_fork, hipEventDisableTiming));
     HIP_CHECK(hipMalloc(&c->d_cnt, sizeof(DevCounters)));
     HIP_CHECK(hipMemset(c->d_cnt, 0, sizeof(DevCounters)));
     HIP_CHECK(hipMalloc(&c->dbg, 16));
@@ -1735,31 +1843,7 @@ int mrt_create(int device, mrt_ctx** out) {
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     c->cus = std::max(1, cus);
     c->trace_grid = (uint32_t)c->cus * 4;  // k_trace_simple (debug)
-    if (const char* e = getenv("MRT_FINISH_PATHS")) c->finish_paths = (uint32_t)std::max(0L, atol(e));
     c->refill_grid = (uint32_t)c->cus * 8;
-    if (const char* e = getenv("MRT_REFILL_KERNEL")) c->refill_kernel = atoi(e) != 0;
-    if (const char* e = getenv("MRT_STATUS_KERNEL")) c->status_kernel = atoi(e) != 0;
-    if (const char* e = getenv("MRT_RESULTS_LOG2")) c->results_max = 1ull << std::max(10, std::min(31, atoi(e)));
-    if (const char* e = getenv("MRT_FINISH_GRID_DIV")) c->finish_grid_div = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    if (getenv("MRT_TRACE_REFILL") || getenv("MRT_TRACE_BOX_MIN")) c->tune_auto_loop = false;
-    if (const char* e = getenv("MRT_TRACE_REFILL")) c->tune.refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    if (const char* e = getenv("MRT_TRACE_PRIM_BATCH")) c->tune.prim_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    if (const char* e = getenv("MRT_SHADE_WPE")) {
-      c->shade_wpe = atoi(e) == 7 ? 7 : 8;
-      c->shade_wpe_auto = false;
-    }
-    if (const char* e = getenv("MRT_TRACE_CHUNK")) {
-      c->tune.chunk = (uint32_t)std::max(64, atoi(e));
-      c->tune_auto_chunk = false;
-    }
-    if (const char* e = getenv("MRT_TRACE_BOX_MIN")) c->tune.box_min = (uint32_t)std::max(1, std::min(65, atoi(e)));
-    if (const char* e = getenv("MRT_SHADE_BATCH")) c->tune.shade_batch = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    if (const char* e = getenv("MRT_POOL_PATHS")) c->pool_paths = (size_t)std::max(1 << 16, std::min(1 << 30, atoi(e)));
-    if (const char* e = getenv("MRT_TRACE_BLOCK")) {
-      const int b = atoi(e);
-      c->trace_block = b >= 1024 ? 1024 : (b >= 512 ? 512 : 256);
-    }
-    if (const char* e = getenv("MRT_TREELET_KB")) c->treelet_kb = (uint32_t)std::max(0, std::min(150, atoi(e)));
   });
   if (rc != MRT_OK) {
     g_last_error = c->err;
@@ -1778,6 +1862,11 @@ extern "C" {
 
 int mrt_destroy(mrt_ctx* c) {
   if (!c) return MRT_OK;
+  if (c->images > 0) {  // an image holds the per-device contexts (massrt.h)
+    c->err = "mrt_destroy: " + std::to_string(c->images) + " image(s) of this context still exist";
+    g_last_error = c->err;
+    return MRT_ERR_STATE;
+  }
   if (c->multi) {
     multi_free(c->multi);
     delete c;
@@ -1789,17 +1878,13 @@ int mrt_destroy(mrt_ctx* c) {
     if (q.stream) hipStreamSynchronize(q.stream);
   hipFree(c->scene_mem);
   hipFree(c->pool_mem);
-  for (int s = 0; s < 2; ++s) {
-    hipFree(c->results_s[s]);
-    if (c->acc_done[s]) hipEventDestroy(c->acc_done[s]);
-    if (c->set_fork[s]) hipEventDestroy(c->set_fork[s]);
-  }
+  hipFree(c->results);
+  if (c->acc_done) hipEventDestroy(c->acc_done);
+  if (c->set_fork) hipEventDestroy(c->set_fork);
   hipFree(c->work);
   hipFree(c->gamma_d);
   for (Queue& q : c->q) {
     hipFree(q.ctrl);
-    if (q.h_status) hipHostFree(q.h_status);
-    if (q.h_work) hipHostFree(q.h_work);
     if (q.h_stat) hipHostFree(q.h_stat);
     for (hipEvent_t e : {q.ev[0], q.ev[1], q.join})
       if (e) hipEventDestroy(e);
@@ -1917,41 +2002,62 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     c->S = S;
     c->scene_bytes = off;
     c->trace_lds = S.n_tlet > 0;
-    // Persistent-loop thresholds per scene (profiles/r2_tune, r3_tune.txt):
-    // a record stream larger than half the chip's L2 (32 MiB over 8 XCDs)
-    // misses to the Infinity Cache, each load round trip is longer, and it
-    // pays to keep more lanes per load instruction (box run while >= 32 lanes
-    // are at a box) and to refill sooner: mesh_ply 438 -> 458, Menger 37.1 ->
-    // 38.2 Msamples/s; L2-resident streams keep 32/24 (sphere_grid 640 vs
-    // 609, cube_field 252 vs 246).
-    if (c->tune_auto_loop) {
-      // round 3, after the box run was unrolled (profiles/r3_tune.txt):
-      // refill 32 everywhere; box run while >= 16 lanes are at a box for an
-      // instance-heavy world (cube_field 266 -> 275, Menger 37.3 -> 44.1),
-      // >= 32 for another stream past half the L2 (mesh_ply 749 -> 775),
-      // else >= 24 (sphere_grid)
-      const bool big = (size_t)S.n_slots * 16 > ((size_t)16 << 20);
-      const bool instanced = S.n_inst > 1000;
-      c->tune.refill = 32u;
-      c->tune.box_min = instanced ? 16u : (big ? 32u : 24u);
-    }
-    // Rays per work grab (round 3, profiles/r3_tune2/, 1024-spp steps): an
-    // L2-resident world without many instances runs longer stretches of
-    // neighbouring rays per wave (camera rays sit together behind the
-    // survivors, §4 Refill): sphere_grid 762.8 / 775.0 / 780.3 / 780.6 at
-    // 128 / 256 / 512 / 1024; mesh_ply 897.4 / 893.1 / 877.8 / 841.4 (its
-    // waves then end on longer tails), so big or instanced worlds keep 128.
-    if (c->tune_auto_chunk) {
-      const bool big = (size_t)S.n_slots * 16 > ((size_t)16 << 20);
-      c->tune.chunk = (big || S.n_inst > 1000) ? 128u : 512u;
-    }
-    if (c->shade_wpe_auto)  // 7 measured on mesh_ply only: instanced worlds keep 8
-      c->shade_wpe = ((size_t)S.n_slots * 16 > ((size_t)16 << 20) && S.n_inst <= 1000) ? 7 : 8;
+    c->scene_big = (size_t)S.n_slots * 16 > ((size_t)16 << 20);
+    c->scene_instances = S.n_inst;
+    apply_options(c);  // the per-scene rules of the options left at -1
     c->tl_boxes = hs.tl_boxes;
     c->scene_alpha = hs.has_alpha;
     c->scene_rng = hs.trav_rng;
     c->scene_ext = !hs.surf_ops.empty() || hs.bg_kind == MRT_BG_CUBEMAP;
     c->has_scene = true;
+  });
+}
+
+int mrt_set_option(mrt_ctx* c, const char* name, int64_t value) {
+  if (c && c->multi && name && !strcmp(name, "gather")) return multi_set_gather(c->multi, value, c->err);
+  MRT_EACH(c, mrt_set_option(c, name, value));
+  return guarded(c, [&] {
+    if (name && !strcmp(name, "gather")) {
+      if (value != MRT_GATHER_AUTO && value != MRT_GATHER_PEER)
+        throw ApiError{MRT_ERR_INVALID, "option gather: a one-device context has no RCCL transport"};
+      return;  // nothing to gather on one device
+    }
+    const int id = opt_find(name);
+    if (id < 0) throw ApiError{MRT_ERR_INVALID, std::string("unknown option ") + (name ? name : "(null)")};
+    set_option(c, id, value);
+    apply_options(c);
+  });
+}
+
+int mrt_get_option(mrt_ctx* c, const char* name, int64_t* value) {
+  if (c && c->multi && name && value && !strcmp(name, "gather")) {
+    *value = multi_gather(c->multi);
+    return MRT_OK;
+  }
+  MRT_DEV0(c, mrt_get_option(c, name, value));
+  return guarded(c, [&] {
+    if (!value) throw ApiError{MRT_ERR_INVALID, "null output"};
+    if (name && !strcmp(name, "gather")) {
+      *value = MRT_GATHER_AUTO;
+      return;
+    }
+    const int id = opt_find(name);
+    if (id < 0) throw ApiError{MRT_ERR_INVALID, std::string("unknown option ") + (name ? name : "(null)")};
+    *value = c->opt[id];
+  });
+}
+
+int mrt_get_tuning(mrt_ctx* c, mrt_tuning* out) {
+  MRT_DEV0(c, mrt_get_tuning(c, out));
+  return guarded(c, [&] {
+    if (!out) throw ApiError{MRT_ERR_INVALID, "null output"};
+    out->queues = (uint32_t)c->n_queues;
+    out->trace_refill = c->tune.refill;
+    out->trace_box_min = c->tune.box_min;
+    out->trace_chunk = c->tune.chunk;
+    out->shade_waves = (uint32_t)c->shade_wpe;
+    out->pool_paths = c->pool_paths;
+    out->results_max = c->results_max;
   });
 }
 

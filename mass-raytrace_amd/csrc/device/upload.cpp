@@ -433,7 +433,7 @@ void put_m4_12(std::vector<float>& dst, const float* m16) {
 
 }  // namespace
 
-bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
+bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err, bool sibling_layout) {
   s = HostScene{};
   SurfResolver surf{d, s, err, {}, {}};
   Emitter e{d, s, err, {}, &surf};
@@ -561,8 +561,7 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err) {
     s.slots[4 * p.first + 2] = r.end;
   }
   if (e.mix_alpha) s.trav_rng = true;
-  const char* lay = getenv("MRT_LAYOUT");  // "dfs": keep the preorder stream (A/B)
-  if (!(lay && !strcmp(lay, "dfs"))) relayout(s);
+  if (sibling_layout) relayout(s);  // false: the plain preorder stream (tools/slab_check.cpp layout check)
   if (s.slots.size() / 4 >= kLdsTag) return (err = "scene too large (record stream >= 2^30 slots)", false);
   return true;
 }

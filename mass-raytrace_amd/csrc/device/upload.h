@@ -51,7 +51,9 @@ struct HostScene {
 };
 
 // Validates the description and linearises it. Returns false with `err` set.
-bool build_host_scene(const mrt_scene_desc& d, HostScene& out, std::string& err);
+// sibling_layout=false keeps every region in plain preorder (the layout
+// before round 2; tools/slab_check.cpp checks both walk alike)
+bool build_host_scene(const mrt_scene_desc& d, HostScene& out, std::string& err, bool sibling_layout = true);
 
 // Chooses the records copied into LDS by every k_trace workgroup (at most
 // `budget` 16-byte slots): the whole stream when it fits; else the small BLAS

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import weakref
 from pathlib import Path
 
 import numpy as np
@@ -26,7 +27,7 @@ LIB_PATH = (Path(_SEL) if _SEL.endswith(".so") else
 REPO = _HERE.parent.parent
 
 # ---- constants (massrt.h) --------------------------------------------------
-ABI_VERSION = 7  # MRT_ABI_VERSION this binding was written for
+ABI_VERSION = 8  # MRT_ABI_VERSION this binding was written for
 REF_NONE, REF_NODE, REF_SPHERE, REF_TRIANGLE, REF_INSTANCE, REF_MODEL, REF_VOLUME = range(7)
 MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_SPECULAR, MAT_ISOTROPHIC, MAT_MIX = range(8)
 WRAP_MIRROR, WRAP_REPEAT, WRAP_CLAMP = range(3)
@@ -147,6 +148,31 @@ class MrtKernelStats(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+class MrtTuning(C.Structure):
+    _fields_ = [("queues", C.c_uint32), ("trace_refill", C.c_uint32), ("trace_box_min", C.c_uint32),
+                ("trace_chunk", C.c_uint32), ("shade_waves", C.c_uint32), ("pool_paths", C.c_uint64),
+                ("results_max", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
+GATHER_AUTO, GATHER_PEER, GATHER_RCCL = 0, 1, 2
+
+
+def env_options(env=None) -> dict:
+    """Options for every Context this process creates, from MASSRT_OPTIONS
+    ("queues=1,treelet_kb=16"): the harness's way for tools/ scripts to A/B a
+    knob through bench.py. The library itself never reads the environment;
+    options reach it only through mrt_set_option."""
+    text = (os.environ if env is None else env).get("MASSRT_OPTIONS", "")
+    out = {}
+    for item in filter(None, (x.strip() for x in text.split(","))):
+        k, _, v = item.partition("=")
+        out[k.strip()] = int(v)
+    return out
+
+
 # scheduling counters of the persistent k_trace (no reference counterpart)
 SCHED_FIELDS = ["wave_slots", "lane_steps", "box_exact", "shaded"]
 
@@ -177,7 +203,7 @@ EXPORTED_SYMBOLS = [
     "mrt_shard_pixels", "mrt_shard_pack_device", "mrt_shard_unpack_device",
     "mrt_create_multi", "mrt_context_devices", "mrt_image_create", "mrt_image_destroy", "mrt_image_clear",
     "mrt_image_render", "mrt_image_prepass", "mrt_image_read", "mrt_image_tonemap", "mrt_image_gather_stats",
-    "mrt_build_info",
+    "mrt_build_info", "mrt_set_option", "mrt_get_option", "mrt_get_tuning", "mrt_context_transport", "mrt_image_gather",
 ]
 
 _lib = None
@@ -263,6 +289,11 @@ def lib() -> C.CDLL:
         "mrt_image_tonemap": (I, [P, U32, C.POINTER(C.c_uint8)]),
         "mrt_image_gather_stats": (I, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
         "mrt_build_info": (C.c_char_p, []),
+        "mrt_set_option": (I, [P, C.c_char_p, I64]),
+        "mrt_get_option": (I, [P, C.c_char_p, C.POINTER(I64)]),
+        "mrt_get_tuning": (I, [P, C.POINTER(MrtTuning)]),
+        "mrt_context_transport": (C.c_char_p, [P]),
+        "mrt_image_gather": (I, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -467,7 +498,7 @@ class Context:
     """One GPU context (mrt_ctx), or one over several devices (devices=[...],
     mrt_create_multi). Raises if no HIP device is present."""
 
-    def __init__(self, device: int = 0, devices=None):
+    def __init__(self, device: int = 0, devices=None, options=None):
         h = C.c_void_p()
         if devices is not None:
             ids = (C.c_int * len(devices))(*devices)
@@ -479,6 +510,28 @@ class Context:
         if rc != 0:
             raise MassrtError(f"{what} failed ({rc}): {lib().mrt_global_last_error().decode()}")
         self.h = h
+        self._images = weakref.WeakSet()  # closed before the context (massrt.h: images first)
+        for k, v in {**env_options(), **(options or {})}.items():
+            self.set_option(k, v)
+
+    def set_option(self, name: str, value: int):
+        """mrt_set_option (massrt.h lists the names); -1 = the per-scene rule where allowed."""
+        self._check(lib().mrt_set_option(self.h, name.encode(), int(value)))
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int64()
+        self._check(lib().mrt_get_option(self.h, name.encode(), C.byref(v)))
+        return int(v.value)
+
+    def tuning(self) -> dict:
+        """The loop's tuning in effect (after the per-scene rules of the last upload)."""
+        t = MrtTuning()
+        self._check(lib().mrt_get_tuning(self.h, C.byref(t)))
+        return t.as_dict()
+
+    def transport(self) -> str:
+        """Gather transport of a multi-device context: "rccl", "peer", "peer (...)" or "none"."""
+        return lib().mrt_context_transport(self.h).decode()
 
     def devices(self) -> list:
         n = C.c_int()
@@ -493,7 +546,11 @@ class Context:
 
     def close(self):
         if self.h:
-            lib().mrt_destroy(self.h)
+            for img in list(self._images):  # an image must not outlive its context
+                img.close()
+            rc = lib().mrt_destroy(self.h)
+            if rc != 0:
+                raise MassrtError(lib().mrt_global_last_error().decode())
             self.h = None
 
     def __del__(self):
@@ -684,6 +741,7 @@ class Image:
         if rc != 0:
             raise MassrtError(lib().mrt_last_error(ctx.h).decode())
         self.h, self.ctx, self.width, self.height = h, ctx, width, height
+        ctx._images.add(self)
 
     def _check(self, rc):
         if rc != 0:
@@ -728,6 +786,11 @@ class Image:
         p = C.c_uint32()
         self._check(lib().mrt_image_read(self.h, _fptr(rgb), b.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(p)))
         return rgb, b, int(p.value)
+
+    def gather(self):
+        """Image::merge at the end of a frame: the devices' tiles onto devices[0]
+        (on the device, no host copy); returns once every device's work has ended."""
+        self._check(lib().mrt_image_gather(self.h))
 
     def tonemap(self, mode: int = 0) -> np.ndarray:
         """Image::to_rgb_bytes + dump's row flip: (H, W, 3) uint8, top row first."""

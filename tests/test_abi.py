@@ -24,7 +24,7 @@ def test_header_symbols_exported():
 
 
 def test_abi_version():
-    assert massrt.lib().mrt_abi_version() == massrt.ABI_VERSION == 7
+    assert massrt.lib().mrt_abi_version() == massrt.ABI_VERSION == 8
 
 
 def test_struct_layouts_match_header(tmp_path):
@@ -39,7 +39,8 @@ def test_struct_layouts_match_header(tmp_path):
                "mrt_surface": massrt.MrtSurface, "mrt_texture": massrt.MrtTexture,
                "mrt_background": massrt.MrtBackground, "mrt_scene_desc": massrt.MrtSceneDesc,
                "mrt_camera": massrt.MrtCamera, "mrt_render_args": massrt.MrtRenderArgs, "mrt_hit": massrt.MrtHit,
-               "mrt_counters": massrt.MrtCounters, "mrt_kernel_stats": massrt.MrtKernelStats}
+               "mrt_counters": massrt.MrtCounters, "mrt_kernel_stats": massrt.MrtKernelStats,
+               "mrt_tuning": massrt.MrtTuning}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{REPO}/include/massrt.h"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')

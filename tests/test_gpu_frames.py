@@ -158,3 +158,70 @@ def test_prepass_then_wavefront_on_one_stream(scene):
     ref = c.render(W, H, 0, 5, seed=7)
     assert _same(out[1][0], ref[0])
     c.close()
+
+
+def test_options_and_tuning(scene, golden_dir):
+    """mrt_set_option / mrt_get_option / mrt_get_tuning (ABI v8): the loop's
+    knobs come from the caller, the per-scene rules fill in -1."""
+    c = massrt.Context(0)
+    assert c.get_option("queues") == 2 and c.get_option("trace_box_min") == -1
+    c.upload(scene)
+    t = c.tuning()
+    assert t["queues"] == 2 and t["trace_box_min"] == 24 and t["trace_chunk"] == 512 and t["shade_waves"] == 8
+    c.set_option("trace_box_min", 40)
+    assert c.tuning()["trace_box_min"] == 40 and c.get_option("trace_box_min") == 40
+    cube = massrt.Builder(1).builtin("cube_field", ASPECT, golden_dir)
+    c.set_option("trace_box_min", -1)
+    c.upload(cube)  # > 1000 instances: box run from 16 lanes, grabs of 128
+    assert c.tuning()["trace_box_min"] == 16 and c.tuning()["trace_chunk"] == 128
+    for name, bad in (("queues", 5), ("trace_block", 300), ("shade_waves", 6), ("trace_chunk", 8)):
+        with pytest.raises(massrt.MassrtError, match=name):
+            c.set_option(name, bad)
+    with pytest.raises(massrt.MassrtError, match="unknown option"):
+        c.set_option("no_such_knob", 1)
+    ref = c.render(W, H, 0, 2, seed=9)
+    c.set_option("queues", 1)  # the pool is re-split: same image
+    assert c.tuning()["queues"] == 1
+    again = c.render(W, H, 0, 2, seed=9)
+    assert _same(ref[0], again[0]) and _same(ref[1], again[1])
+    c.close()
+
+
+def test_transport_and_image_lifetime(scene):
+    one = _ctx(scene)
+    multi = _ctx(scene, devices=[0, 0])
+    assert one.transport() == "none" and multi.transport() == "peer"
+    with pytest.raises(massrt.MassrtError, match="distinct devices"):
+        multi.set_option("gather", massrt.GATHER_RCCL)
+    img = massrt.Image(multi, W, H)
+    img.render(1, 0, 2)
+    assert img.passes == 2
+    assert img.gather_stats()[0] == 0  # the pass count alone gathers nothing (ADVICE r3)
+    img.gather()
+    assert img.gather_stats()[0] == 16 * massrt.shard_pixels(W, H, 1, 2).size
+    # an image must be destroyed before its context: mrt_destroy refuses
+    assert massrt.lib().mrt_destroy(multi.h) == 4  # MRT_ERR_STATE
+    assert "image" in massrt.lib().mrt_last_error(multi.h).decode()
+    multi.close()  # closes the image first
+    assert img.h is None and multi.h is None
+    one.close()
+
+
+def test_constrained_memory_renders_in_chunks(scene):
+    """a render sizes its pool and results slab to the free device
+    memory minus mem_reserve_mb (several contexts may share a device). With
+    almost no memory left to it, a multi-device context over repeated devices
+    shrinks the pool and the samples per chunk — and renders the same image."""
+    import torch
+
+    Wl, Hl, spp = 640, 360, 24
+    one = _ctx(scene)
+    ref = one.render(Wl, Hl, 0, spp, seed=12)
+    one.close()
+    free_mb = torch.cuda.mem_get_info(0)[0] >> 20
+    multi = massrt.Context(devices=[0, 0, 0], options={"mem_reserve_mb": max(0, free_mb - 300)})
+    multi.upload(scene)
+    got = multi.render(Wl, Hl, 0, spp, seed=12)
+    t = multi.tuning()
+    multi.close()
+    assert _same(ref[0], got[0]) and _same(ref[1], got[1]), t

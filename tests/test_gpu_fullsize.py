@@ -74,9 +74,9 @@ def textured(assets_dir):
             oracle.Scene(1).builtin("mesh_obj_textured", ASPECT, assets_dir))
 
 
-def test_4k_pixel_subset_across_result_chunks(monkeypatch, textured):
+def test_4k_pixel_subset_across_result_chunks(textured):
     """144 spp of the 4K frame = 1.19G samples. The results slab holds 2^31
-    samples by default (258 spp of 8.3M pixels); with MRT_RESULTS_LOG2=30 the
+    samples by default (258 spp of 8.3M pixels); with results_log2 = 30 the
     library splits this call into chunks of 2^30 samples (129 spp), so it
     crosses a chunk boundary. A pixel subset must match the oracle (bounces
     bit-exact; radiance within 1e-4: acos/atan2 of SkySphere are ocml vs
@@ -84,8 +84,7 @@ def test_4k_pixel_subset_across_result_chunks(monkeypatch, textured):
     bit, and neither must the default slab (one chunk)."""
     b, o = textured
     spp = 144
-    monkeypatch.setenv("MRT_RESULTS_LOG2", "30")
-    c = massrt.Context(0)
+    c = massrt.Context(0, options={"results_log2": 30})
     try:
         c.upload(b)
         rgb, bo = c.render(W4, H4, 0, spp, seed=5)
@@ -93,7 +92,6 @@ def test_4k_pixel_subset_across_result_chunks(monkeypatch, textured):
         part = c.render(W4, H4, 129, spp - 129, seed=5, accum=part)
     finally:
         c.close()
-    monkeypatch.delenv("MRT_RESULTS_LOG2")
     px = np.arange(3, W4 * H4, 15_013, dtype=np.uint32)
     orgb, obo = o.render_pixels(W4, H4, px, 0, spp, seed=5)
     assert np.array_equal(bo[px], obo)
@@ -123,7 +121,7 @@ def test_4k_deterministic_and_shard_additive(ctx, textured):
 
 
 @pytest.mark.parametrize("scene", ["sphere_grid", "cube_field", "mesh_ply"])
-def test_fullsize_treelet_equals_plain(golden_dir, assets_dir, monkeypatch, scene):
+def test_fullsize_treelet_equals_plain(golden_dir, assets_dir, scene):
     """k_trace with the LDS treelet and parked global loads (1024 threads,
     78 KB) renders full 1080p frames bit-identical to the plain kernel: many
     refills per lane, both queues, every lane state transition at scale."""
@@ -131,9 +129,7 @@ def test_fullsize_treelet_equals_plain(golden_dir, assets_dir, monkeypatch, scen
     spp = 1 if scene == "mesh_ply" else 2
     out = []
     for block, kb in ((256, 0), (1024, 78)):
-        monkeypatch.setenv("MRT_TRACE_BLOCK", str(block))
-        monkeypatch.setenv("MRT_TREELET_KB", str(kb))
-        c = massrt.Context(0)
+        c = massrt.Context(0, options={"trace_block": block, "treelet_kb": kb})
         try:
             c.upload(b)
             out.append(c.render(W, H, 0, spp, seed=5))

@@ -323,50 +323,25 @@ def test_tiny_coordinates_keep_the_early_decision(ctx):
 
 
 @pytest.mark.parametrize("scene", ["sphere_grid", "cube_field"])
-def test_drain_handoff_is_bit_identical(small_scenes, monkeypatch, scene):
+def test_drain_handoff_is_bit_identical(small_scenes, scene):
     """A queue whose work is exhausted hands its last paths to the fused
     kernel in adopt mode (render.hip launch_finish_v): the image must be
-    the per-bounce wavefront's bit for bit — never, at once, by default."""
+    the per-bounce wavefront's bit for bit — never, at once, by default
+    (option finish_paths)."""
     b, _ = small_scenes[scene]
     out = []
-    for v in ("0", "1000000000", None):
-        if v is None:
-            monkeypatch.delenv("MRT_FINISH_PATHS", raising=False)
-        else:
-            monkeypatch.setenv("MRT_FINISH_PATHS", v)
+    for v in (0, 1000000000, None):
         c = massrt.Context(0)
+        if v is not None:
+            c.set_option("finish_paths", v)
         c.upload(b)
         c.reset_kernel_stats()
         out.append(c.render(64, 36, 0, 16, seed=11, flags=massrt.RENDER_TIME_KERNELS))
-        if v == "1000000000":
+        if v == 1000000000:
             assert c.kernel_stats()["finish_launches"] > 0
         c.close()
     for rgb, bo in out[1:]:
         assert np.array_equal(out[0][0].view(np.uint32), rgb.view(np.uint32)) and np.array_equal(out[0][1], bo)
-
-
-def test_queue_sets_option_is_bit_identical(small_scenes, monkeypatch):
-    """MRT_QUEUE_SETS=2: consecutive render calls alternate between two queue
-    sets (pools, work counters, result slabs) and a call returns while its
-    set may still drain; accumulation order into the caller's buffer, hence
-    the image, must not change."""
-    b, _ = small_scenes["sphere_grid"]
-    W, H = 64, 36
-    monkeypatch.delenv("MRT_QUEUE_SETS", raising=False)
-    c = massrt.Context(0)
-    c.upload(b)
-    ref = c.render(W, H, 0, 12, seed=13)
-    c.close()
-    monkeypatch.setenv("MRT_QUEUE_SETS", "2")
-    c = massrt.Context(0)
-    c.upload(b)
-    acc = (np.zeros(W * H * 3, np.float32), np.zeros(W * H, np.uint32))
-    for s0 in (0, 4, 8):
-        acc = c.render(W, H, s0, 4, seed=13, accum=acc)
-    whole = c.render(W, H, 0, 12, seed=13)
-    c.close()
-    for rgb, bo in (acc, whole):
-        assert np.array_equal(ref[0].view(np.uint32), rgb.view(np.uint32)) and np.array_equal(ref[1], bo)
 
 
 def test_errors_are_reported(ctx):
@@ -633,14 +608,12 @@ def test_menger_parity(ctx, assets_dir, scene):
 
 
 @pytest.mark.parametrize("block,kb", [(256, 0), (256, 1), (256, 4), (256, 24), (512, 48), (1024, 78), (1024, 150)])
-def test_treelet_budgets_bit_exact(golden_dir, monkeypatch, block, kb):
+def test_treelet_budgets_bit_exact(golden_dir, block, kb):
     """The LDS treelet (upload.cpp build_treelet) at several budgets and
     workgroup sizes: no treelet, a few boxes, the top of the trees, small
     BLAS regions whole, whole small scenes. Closest hits and traversal
     counters must equal the oracle's for every choice of copied records."""
-    monkeypatch.setenv("MRT_TRACE_BLOCK", str(block))
-    monkeypatch.setenv("MRT_TREELET_KB", str(kb))
-    c = massrt.Context(0)
+    c = massrt.Context(0, options={"trace_block": block, "treelet_kb": kb})
     try:
         for scene in SMALL:
             b = massrt.Builder(1).builtin(scene, ASPECT, golden_dir)

@@ -1,5 +1,5 @@
 """The record-stream layout (layout.h, upload.cpp relayout_blas) on the host,
-no GPU: the same rays through the preorder stream (MRT_LAYOUT=dfs) and
+no GPU: the same rays through the preorder stream (build_host_scene(..., sibling_layout=false)) and
 through the default layout (BLAS regions with siblings together, every
 successor explicit) find the same closest hits, t bits included, after the
 same number of box tests; the early slab decision stays exact

@@ -8,8 +8,8 @@
 #   bash tools/gpu_session.sh profile SCENE...      # rocprofv3 stats + stamped PMC (tools/profile.sh)
 #   bash tools/gpu_session.sh configs               # every BASELINE config scene, timing only
 #   LABELS="a b" LIBS="x.so y.so" bash tools/gpu_session.sh ab   # bench per library build (MASSRT_LIB)
-#   SWEEP=$'base\ntl MRT_TREELET_KB=16' bash tools/gpu_session.sh sweep   # bench per env configuration
-#   bash tools/gpu_session.sh rehearse              # bench.py --gpus 2 (gloo) on one GPU
+#   SWEEP=$'base\ntl MASSRT_OPTIONS=treelet_kb=16' bash tools/gpu_session.sh sweep   # bench per option set
+#   bash tools/gpu_session.sh rehearse              # bench.py --gpus 2 --devices 0,0 (one process, peer gather)
 # SCENES (default "sphere_grid mesh_ply") and STEPS (default 3) apply to ab / sweep / args;
 # BENCH_ARGS (e.g. "--spp-per-step 1024") is appended to every sweep run.
 set -o pipefail
@@ -25,7 +25,7 @@ print('%-28s %-12s %8.1f Msamples/s  %8.1f ms/step  k_trace %.3f ms  k_shade %.3
 }
 quick() {  # label, log, bench args...: a timing-only bench of one scene
   local label=$1 log=$2; shift 2
-  timeout -k 10 400 python bench.py --secondary none --no-cpu-baseline --no-dropin "$@" > $log 2>&1 || { echo "FAILED $label"; tail -5 $log; return 1; }
+  timeout -k 10 400 python bench.py --secondary none --no-cpu-baseline --no-dropin --no-configs "$@" > $log 2>&1 || { echo "FAILED $label"; tail -5 $log; return 1; }
   line $log $label
 }
 
@@ -62,7 +62,7 @@ case $MODE in
       set -- $cfg; lab=$1; shift
       for sc in $SCENES; do
         log=gpurun_out/session/sweep_${lab}_$sc.log
-        env "$@" timeout -k 10 400 python bench.py --scene $sc --secondary none --no-cpu-baseline --no-dropin \
+        env "$@" timeout -k 10 400 python bench.py --scene $sc --secondary none --no-cpu-baseline --no-dropin --no-configs \
           --steps $STEPS $BENCH_ARGS > $log 2>&1 || { echo "FAILED $lab $sc"; tail -5 $log; exit 1; }
         line $log $lab
       done
@@ -75,9 +75,9 @@ case $MODE in
         quick "$lab" gpurun_out/session/args_${lab}_$sc.log --scene $sc --steps $STEPS "$@" || exit 1
       done
     done <<< "$ARGSETS" ;;
-  rehearse)  # N>1 without a launcher on the 1-GPU box: both ranks on device 0, gloo staging the slabs
-    MRT_POOL_PATHS=134217728 timeout -k 10 600 python -u bench.py --gpus 2 --dist-backend gloo --spp-per-step 256 \
-      --steps 2 --secondary none --no-cpu-baseline --no-dropin > gpurun_out/session/rehearse2.log 2>&1 &&
-    tail -1 gpurun_out/session/rehearse2.log | cut -c1-400 ;;
+  rehearse)  # N=2 on the 1-GPU box: one process, one context over devices {0,0}, peer-copy gather
+    timeout -k 10 600 python -u bench.py --gpus 2 --devices 0,0 --steps 2 --secondary none --no-cpu-baseline \
+      --no-dropin --no-configs > gpurun_out/session/rehearse2.log 2>&1 &&
+    tail -1 gpurun_out/session/rehearse2.log | cut -c1-600 ;;
   *) echo "unknown mode $MODE"; exit 2 ;;
 esac

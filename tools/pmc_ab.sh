@@ -1,7 +1,7 @@
 #!/bin/bash
-# PMC comparison of env configurations on one scene (1 bench step each):
+# PMC comparison of option sets (MASSRT_OPTIONS) on one scene (1 bench step each):
 # TA busy / wavefronts, TCP accesses, LDS and VMEM instruction counts.
-#   SCENE=sphere_grid CONFIGS="base:MRT_TREELET_KB=0;tl:MRT_TREELET_KB=16" bash tools/pmc_ab.sh
+#   SCENE=sphere_grid CONFIGS="base:MASSRT_OPTIONS=treelet_kb=0;tl:MASSRT_OPTIONS=treelet_kb=16" bash tools/pmc_ab.sh
 set -o pipefail
 export TMPDIR=/tmp
 SCENE=${SCENE:-sphere_grid}
@@ -14,7 +14,7 @@ for c in "${CFGS[@]}"; do
              "SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_WAVES"; do
     tag=$(echo $grp | cut -c1-6)
     env $envs timeout -k 10 240 rocprofv3 --pmc $grp -d $OUT/${label}_$tag -o run --output-format csv -- \
-      python3 bench.py --scene $SCENE --secondary none --no-cpu-baseline --steps 1 --warmup 1 --no-kernel-timing \
+      python3 bench.py --scene $SCENE --secondary none --no-cpu-baseline --no-configs --no-dropin --steps 1 --warmup 1 --no-kernel-timing \
       > $OUT/${label}_$tag.log 2>&1 || { echo "pmc $label failed"; tail -5 $OUT/${label}_$tag.log; exit 1; }
   done
   echo "== $label ($envs)"

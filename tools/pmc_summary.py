@@ -117,7 +117,7 @@ import os  # noqa: E402
 tag = os.environ.get("PMC_TAG", "")
 if tag:
     summary["tag"] = tag
-    summary["env"] = {k: v for k, v in os.environ.items() if k.startswith("MRT_")}
+    summary["options"] = os.environ.get("MASSRT_OPTIONS", "")
 for dst in (REPO / "profiles" / f"pmc_{scene}{tag}.json", out_dir / f"pmc_{scene}{tag}.json"):  # out_dir: travels back
     dst.write_text(json.dumps(summary, indent=1))
     print("wrote", dst)

@@ -7,10 +7,10 @@
 set -o pipefail
 export TMPDIR=/tmp
 SCENE=${SCENE:-sphere_grid}
-TAG=${TAG:-}   # e.g. TAG=_solo with MRT_QUEUES=1: profiles/pmc_<scene>_solo.json (not read by bench.py)
+TAG=${TAG:-}   # e.g. TAG=_solo with MASSRT_OPTIONS=queues=1: profiles/pmc_<scene>_solo.json
 OUT=gpurun_out/prof_$SCENE$TAG
 rm -rf $OUT; mkdir -p $OUT
-B="bench.py --scene $SCENE --no-cpu-baseline --no-dropin --secondary none"
+B="bench.py --scene $SCENE --no-cpu-baseline --no-dropin --no-configs --secondary none"
 P="--steps 1 --warmup 1 --no-kernel-timing"
 run() {  # name, timeout, rocprofv3 args...
   local name=$1 t=$2; shift 2

@@ -202,15 +202,13 @@ int main(int argc, char** argv) {
     printf("%s\n", err.c_str());
     return 1;
   }
-  // `layout` mode: the same rays through the preorder stream (MRT_LAYOUT=dfs)
+  // `layout` mode: the same rays through the plain preorder stream (build_host_scene(..., false))
   // and the default layout (BLAS regions with siblings together) must find the
   // same closest hits, t bits included, after the same number of box tests
   HostScene dfs;
   const bool layout = argc > 4 && !strcmp(argv[4], "layout");
   if (layout) {
-    setenv("MRT_LAYOUT", "dfs", 1);
-    if (!build_host_scene(d, dfs, err)) return 1;
-    unsetenv("MRT_LAYOUT");
+    if (!build_host_scene(d, dfs, err, false)) return 1;
   }
   uint64_t layout_bad = 0;
   std::mt19937 g(7);

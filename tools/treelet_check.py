@@ -18,8 +18,7 @@ _, cam = b.desc()
 rays = {"cam2M": camera_rays(cam, 1 << 21, 3), "rand2M": random_rays(1 << 21, 4)}
 res = []
 for blk, k in (("256", "0"), (block, kb)):
-    os.environ["MRT_TRACE_BLOCK"], os.environ["MRT_TREELET_KB"] = blk, k
-    c = massrt.Context(0)
+    c = massrt.Context(0, options={"trace_block": int(blk), "treelet_kb": int(k)})
     c.upload(b)
     r = {name: c.trace_rays(v) for name, v in rays.items()}
     for cnt in (False, True):
