@@ -262,6 +262,7 @@ pub struct mrt_counters {
     pub lane_steps: u64,
     pub box_exact: u64,
     pub shaded: u64,
+    pub vnf_fallbacks: u64,
 }
 
 #[repr(C)]
@@ -293,7 +294,12 @@ pub struct mrt_tuning {
     pub shade_waves: u32,
     pub pool_paths: u64,
     pub results_max: u64,
+    pub traversal: u32,
 }
+
+/// Context option "traversal" (ABI v8).
+pub const MRT_TRAVERSAL_REFERENCE: i64 = 0;
+pub const MRT_TRAVERSAL_NEAR_FIRST: i64 = 1;
 
 /// Opaque handles.
 #[repr(C)]

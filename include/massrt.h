@@ -259,6 +259,9 @@ typedef struct {
   /* paths k_shade advanced (one per traced segment shaded by the wavefront
      loop; the drain hand-off's fused launches shade the rest; ABI v7) */
   uint64_t shaded;
+  /* near-first walks whose hit the reference's walk would not reach: walked
+     again the reference's way (ABI v8) */
+  uint64_t vnf_fallbacks;
 } mrt_counters;
 
 /* Kernel timing accumulated by renders flagged MRT_RENDER_TIME_KERNELS
@@ -334,9 +337,22 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  *   trace_block       256, 512, 1024  k_trace workgroup beside a treelet
  *   mem_reserve_mb    device memory a render leaves free (default 4096)
  *   gather            MRT_GATHER_* (multi-device contexts)
+ *   traversal         MRT_TRAVERSAL_* (default REFERENCE); NEAR_FIRST applies
+ *                     to scenes without traversal draws (Volume, Mix alpha)
+ *                     and without a treelet, others keep REFERENCE
  * Every render sizes its path pool and results slab to the device memory
  * free at that moment minus mem_reserve_mb (several contexts may share a
  * device), shrinking the pool first and then the samples per chunk. */
+/* How k_trace finds each closest hit (geom.rs:185-205 BvhNode::intersect):
+ * REFERENCE walks the reference's tree left child first (the reference's own
+ * sequence of box and primitive tests); NEAR_FIRST walks surface-area-
+ * heuristic trees over the same primitives near child first, then checks
+ * that the reference's walk reaches the hit it found (its innermost reference
+ * ancestors pass BoundingBox::hit at that t) and walks the reference's way
+ * where it does not — the same closest hits, ties included, from fewer box
+ * tests. Counters (node visits, ...) then count its work. */
+#define MRT_TRAVERSAL_REFERENCE 0
+#define MRT_TRAVERSAL_NEAR_FIRST 1
 #define MRT_GATHER_AUTO 0 /* RCCL between distinct devices, peer copies otherwise */
 #define MRT_GATHER_PEER 1 /* HIP peer copies */
 #define MRT_GATHER_RCCL 2 /* RCCL send/recv (distinct devices only) */
@@ -346,6 +362,7 @@ int mrt_get_option(mrt_ctx* ctx, const char* name, int64_t* value);
 typedef struct {
   uint32_t queues, trace_refill, trace_box_min, trace_chunk, shade_waves;
   uint64_t pool_paths, results_max;
+  uint32_t traversal; /* the walk k_trace uses for this scene (MRT_TRAVERSAL_*) */
 } mrt_tuning;
 int mrt_get_tuning(mrt_ctx* ctx, mrt_tuning* out);
 

@@ -52,6 +52,37 @@ enum : uint32_t { TRI_FLAG_ALPHA = 1u, TRI_FLAG_UV = 2u };  // tri_shade flags
 constexpr uint32_t kTriAlpha = 0x80000000u;
 constexpr uint32_t kTriIdMask = 0x0FFFFFFFu;
 
+// ---- verified near-first trees (round 4, nf_tree.cpp, path.h trav_*_nf) ----
+// A second set of trees over the same primitives, appended to the slot
+// array after the reference stream: a surface-area-heuristic BVH over the
+// world's objects (spheres, instances, models, world triangles) and one per
+// BLAS, walked near child first with a per-lane stack (k_trace's NF variant).
+// The walk finds the closest hit with the reference's tie rule (the later
+// primitive in the reference's left-first order wins, keys below), then the
+// winner is checked against the REFERENCE tree (its two innermost reference
+// ancestors must pass BoundingBox::hit at the winning t — nested boxes, so the
+// outer ones do too — i.e. the reference's left-first walk reaches it); a ray
+// that fails the check is traced again the reference's way.
+//   NF BOX  2 slots {min.x,min.y,min.z,max.x} {max.y,max.z,right,kBoxFlag|axis<<28|left}
+//           axis 0..2: the near child is left when d[axis] >= 0, else right;
+//           axis 3 (kNfLeaf): a leaf, `left` = its first primitive record
+//   SPHERE / TRI as in the reference stream, `next` = the leaf's following
+//           record or kNfPop (continue with the stack)
+//   INST / MODEL {id, nf_blas_root, next, 0} {0,0,0,INST|MODEL}
+constexpr uint32_t kNfIdx = 0x0FFFFFFFu;  // index bits of an NF box's left child
+constexpr uint32_t kNfPop = 0x0FFFFFFFu;  // "next" of a leaf's last record: pop the stack
+constexpr uint32_t kNfLeaf = 3u;           // axis field of a leaf box
+constexpr uint32_t kNfStack = 24u;         // stack entries per lane (LDS): the trees' depth is capped to fit
+constexpr uint32_t kNoParent = 0xFFFFFFFFu;
+// Verification record of a leaf object (DevScene::vnf_leaf[vnf_base[kind] + id]):
+//   {reference parent box record (kNoParent: a root object), order key}
+// order key: the object's position among the reference's leaves of its
+// region, left-first — the world region for spheres, instances, models and
+// world triangles; its BLAS for a model's triangles (kWorldKey set: a world
+// triangle, whose key is a world key)
+constexpr uint32_t kWorldKey = 0x80000000u;
+enum : uint32_t { VNF_SPHERE = 0, VNF_TRI = 1, VNF_INST = 2, VNF_MODEL = 3 };
+
 // Composite surfaces (YCbCrTexture, TextureBlend, SolidColorFallback,
 // texture.rs:197-357) run as small postfix programs over a V4 stack:
 //   SOLID    push color                TEXTURE  push get_f(tex)
@@ -130,6 +161,11 @@ struct DevScene {
   const uint32_t* tlet;        // the treelet image copied into LDS (n_tlet slots of 4 words)
   uint32_t n_tlet;
   uint32_t tl_world_begin;     // world entry index beside the treelet (possibly LDS-tagged)
+  // verified near-first trees (nf_ok == 0: the scene has none)
+  uint32_t nf_ok, nf_world;    // the NF world tree's root record
+  const uint32_t* vnf_leaf;    // {reference parent box, order key} pairs per leaf object
+  uint32_t vnf_base[4];        // first vnf_leaf entry of spheres, triangles, instances, models
+  uint32_t n_vnf;
 };
 
 }  // namespace mrt

@@ -27,12 +27,12 @@ MRT_DEV uint32_t make_ref(uint32_t kind, uint32_t idx) { return (kind << 28) | i
 
 struct DevCounters {
   unsigned long long samples, segments, node_visits, sphere_tests, triangle_tests, instance_entries,
-      model_entries, closest_hits, texel_taps, bounces, wave_slots, lane_steps, box_exact, shaded;
+      model_entries, closest_hits, texel_taps, bounces, wave_slots, lane_steps, box_exact, shaded, vnf_fallbacks;
 };
 
 struct LocalCounters {
   uint32_t node_visits = 0, sphere_tests = 0, triangle_tests = 0, instance_entries = 0, model_entries = 0,
-           texel_taps = 0, wave_slots = 0, lane_steps = 0, box_exact = 0;
+           texel_taps = 0, wave_slots = 0, lane_steps = 0, box_exact = 0, vnf_fallbacks = 0;
 };
 
 // Bounds checks of every scene-array index, compiled in with
@@ -377,6 +377,7 @@ struct TravIn {
   const float4* rd;        // ray directions (xyz)
   float tmin;
   uint4* rng = nullptr;    // the rays' RNG states (traversal draws: Volume, Mix alpha tests)
+  float tmax0 = INFINITY;  // the walk's initial t_max (a near-first lane that falls back restarts with it)
 };
 
 // Inside a BLAS, `ret` is the world record after the instance/model record
@@ -384,6 +385,7 @@ struct TravIn {
 // hit is recovered from that record when the ray finishes (trav_hit).
 constexpr uint32_t kNoRet = 0xFFFFFFFFu;
 constexpr uint32_t kRetInstance = 0x80000000u;
+constexpr uint32_t kExactModeInit = 0xFFFFu;  // Trav::sp of the reference's walk (= kExactMode below)
 
 struct Trav {
   TRay r;  // ray of the space being traversed (world, or instance object space)
@@ -393,6 +395,8 @@ struct Trav {
   uint32_t prim, hit_ret;  // closest hit so far: primitive (kRefNone: none) and `ret` when found
   uint4 s0, s1;  // current record (prefetched when i moves)
   PathRng rng;   // the ray's stream, for scenes whose traversal draws (RNG variants only)
+  uint32_t sp;   // near-first walk: stack entries in use (kExactMode: the reference's walk)
+  float t2;      // near-first walk: the smallest t of the other hits it met (nf_finish)
   bool done;
 #ifdef MRT_DEBUG_BOUNDS
   uint32_t steps;
@@ -546,7 +550,7 @@ MRT_DEV void trav_end_index(const TravIn& in, Trav& t) {
 
 // Start ray `ray` of the pool (World::intersect(ray, in.tmin, tmax)).
 template <bool RNG = false, bool LDS = false>
-MRT_DEV void trav_init(const TravIn& in, Trav& t, uint32_t ray, float tmax) {
+MRT_DEV void trav_init(const TravIn& in, Trav& t, uint32_t ray, float tmax, uint32_t start = 0xFFFFFFFFu) {
   if (RNG) {
     const uint4 q = in.rng[ray];
     t.rng = PathRng{(unsigned long long)q.x | ((unsigned long long)q.y << 32),
@@ -554,7 +558,9 @@ MRT_DEV void trav_init(const TravIn& in, Trav& t, uint32_t ray, float tmax) {
   }
   t.r = world_ray(in, ray);
   t.ray = ray;
-  t.i = in.world_begin;
+  t.i = start == 0xFFFFFFFFu ? in.world_begin : start;  // the near-first walk starts at its own world tree
+  t.sp = start == 0xFFFFFFFFu ? kExactModeInit : 0u;
+  t.t2 = INFINITY;
   t.ret = kNoRet;
   t.best = tmax;
   t.prim = kRefNone;
@@ -679,6 +685,212 @@ template <bool COUNT, uint32_t ALPHA, bool RNG = false, bool LDS = false>
 MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
   trav_prim_index<COUNT, ALPHA, RNG, LDS>(in, t, lc);
   if (!t.done) trav_fetch<LDS>(in, t);
+}
+
+// ---- verified near-first walk (layout.h, nf_tree.cpp; k_trace<..., NF>) ------
+// The lane walks the SAH trees near child first with a stack of record
+// indices in LDS (kNfStack entries per lane, stride BLK), finds the closest
+// hit with the reference's tie rule, then checks that the reference's
+// left-first walk reaches that hit; if not it walks again the reference's
+// way (sp = kExactMode: trav_box_index / trav_prim_index on the reference
+// stream, the exact kernel's steps). Boxes are culled at best * (1 + 2^-10):
+// a primitive whose computed t undercuts its box's computed entry by less
+// than that is still found.
+constexpr uint32_t kExactMode = kExactModeInit;
+constexpr uint32_t kNfDone = 0xFFFEu;     // Trav::sp: the near-first walk is over, its hit not yet checked
+constexpr uint32_t kNfRet = 0x80000000u;  // stack marker: leave the BLAS (back to the world ray)
+
+struct NfStack {
+  uint32_t* p;  // this lane's entry 0 (LDS)
+  uint32_t stride;
+};
+MRT_DEV void nf_push(const NfStack& k, Trav& t, uint32_t v) {
+  k.p[t.sp * k.stride] = v;
+  t.sp += 1;  // the builder bounds the depth (nf_stack_need <= kNfStack)
+}
+// next record from the stack; false: the walk is over
+MRT_DEV bool nf_pop(const TravIn& in, const NfStack& k, Trav& t) {
+  for (;;) {
+    if (t.sp == 0) return false;
+    t.sp -= 1;
+    const uint32_t v = k.p[t.sp * k.stride];
+    if (v != kNfRet) {
+      t.i = v;
+      return true;
+    }
+    if (t.ret & kRetInstance) t.r = world_ray(in, t.ray);  // a model shares the world ray
+    t.ret = kNoRet;
+  }
+}
+MRT_DEV uint32_t vnf_entry(const DevScene& S, uint32_t base, uint32_t id, uint32_t word) {
+  return S.vnf_leaf[2 * (size_t)MRT_IDX(S, S.vnf_base[base] + id, S.n_vnf, 23) + word];
+}
+// the reference's order of primitive occurrence (prim, ret): {world key, BLAS key}
+MRT_DEV unsigned long long nf_key(const TravIn& in, uint32_t prim, uint32_t ret) {
+  const DevScene& S = in.S;
+  const uint32_t kind = prim >> 28, id = prim & 0x0FFFFFFFu;
+  if (kind == MRT_REF_SPHERE) return (unsigned long long)vnf_entry(S, VNF_SPHERE, id, 1) << 32;
+  const uint32_t k = vnf_entry(S, VNF_TRI, id, 1);
+  if (k & kWorldKey) return (unsigned long long)(k & ~kWorldKey) << 32;
+  const uint32_t rec = (ret & ~kRetInstance) - 2;  // the NF instance/model record (layout.h)
+  const uint32_t cid = in.slots[MRT_IDX(S, rec, S.n_slots, 24)].x;
+  const uint32_t wk = vnf_entry(S, (ret & kRetInstance) ? VNF_INST : VNF_MODEL, cid, 1);
+  return ((unsigned long long)wk << 32) | k;
+}
+// does a hit (th, prim, current ret) replace the best so far? (t_max is
+// inclusive in the reference: an equal t goes to the later primitive)
+MRT_DEV bool nf_better(const TravIn& in, const Trav& t, float th, uint32_t prim) {
+  if (th < t.best) return true;
+  if (!(th == t.best)) return false;
+  if (t.prim == kRefNone) return true;
+  return nf_key(in, prim, t.ret) > nf_key(in, t.prim, t.hit_ret);
+}
+MRT_DEV float nf_cull(float best) { return fmaf(fabsf(best), 0x1p-10f, best); }
+// a hit at th (<= the culling bound): the new best, or one of the other hits (t2)
+MRT_DEV void nf_hit(const TravIn& in, Trav& t, float th, uint32_t prim) {
+  if (th <= t.best && nf_better(in, t, th, prim)) {
+    t.t2 = fminf(t.t2, t.best);
+    t.best = th;
+    t.prim = prim;
+    t.hit_ret = t.ret;
+  } else {
+    t.t2 = fminf(t.t2, th);
+  }
+}
+// the walk is over: k_trace checks the hit once per loop iteration (nf_finish);
+// until then the lane holds an END record, never a box (the box-run ballot)
+MRT_DEV void nf_over(Trav& t) {
+  t.sp = kNfDone;
+  t.s1.w = KIND_END;
+}
+
+// The reference's box test of reference record `rec` (a box) at t_max = t.
+MRT_DEV bool ref_box_hits(const TravIn& in, uint32_t rec, const TRay& r, float t) {
+  uint4 a, b;
+  rec_load2<false>(in, rec, a, b);
+  return box_hit_any(V3{u2f(a.x), u2f(a.y), u2f(a.z)}, V3{u2f(a.w), u2f(b.x), u2f(b.y)}, r, in.tmin, t);
+}
+
+// The near-first walk is over: does the reference's left-first walk reach
+// the winner? The reference enters an ancestor box B of the winner iff
+// BoundingBox::hit(B, t_max) holds for its t_max when it gets there, which is
+// the smallest t of the hits it accepted BEFORE B — other hits than the
+// winner, so at least tau = min(t2, best * (1 + 2^-10)) (t2: the other hits
+// this walk met; any hit it did not meet lies beyond the culling margin).
+// BoundingBox::hit is monotone in t_max, so B passing at tau suffices; the
+// reference's boxes are nested, so the winner's world parent (world ray) and,
+// inside a BLAS, its BLAS parent (that space's ray) stand for all of them.
+// Yes: the ray is done (its record set to END for k_trace's box-run ballot).
+// No: the reference's walk from the start (kExactMode).
+template <bool COUNT>
+MRT_DEV void nf_finish(const TravIn& in, Trav& t, LocalCounters& lc) {
+  const DevScene& S = in.S;
+  bool ok = true;
+  const float tau = fminf(t.t2, nf_cull(t.best));
+  if (t.prim != kRefNone) {
+    const uint32_t kind = t.prim >> 28, id = t.prim & 0x0FFFFFFFu;
+    const uint32_t own = vnf_entry(S, kind == MRT_REF_SPHERE ? VNF_SPHERE : VNF_TRI, id, 0);
+    if (t.hit_ret == kNoRet) {  // a world object (t.r is the world ray: every BLAS was left)
+      if (own != kNoParent) ok = ref_box_hits(in, own, t.r, tau);
+    } else {
+      const bool inst = (t.hit_ret & kRetInstance) != 0;
+      const uint32_t cid = in.slots[MRT_IDX(S, (t.hit_ret & ~kRetInstance) - 2, S.n_slots, 24)].x;
+      const uint32_t wpar = vnf_entry(S, inst ? VNF_INST : VNF_MODEL, cid, 0);
+      if (wpar != kNoParent) ok = ref_box_hits(in, wpar, t.r, tau);
+      if (ok && own != kNoParent) {
+        TRay r = t.r;
+        if (inst) {
+          V3 c0, c1, c2, c3;
+          load_m12(S.inst_inv + (size_t)MRT_IDX(S, cid, S.n_inst, 8) * 12, c0, c1, c2, c3);
+          r = make_tray(xform(c0, c1, c2, c3, t.r.o, 1.0f), xform(c0, c1, c2, c3, t.r.d, 0.0f), S.fast_ok);
+        }
+        ok = ref_box_hits(in, own, r, tau);
+      }
+      if (COUNT) lc.node_visits += 1;
+    }
+    if (COUNT) lc.node_visits += 1;
+  }
+  if (ok) {
+    t.done = true;
+    t.s1.w = KIND_END;  // a done lane holds an END record (k_trace's box-run ballot)
+    return;
+  }
+  if (COUNT) lc.vnf_fallbacks++;
+  t.sp = kExactMode;  // the reference's walk (the caller fetches t.i)
+  t.i = in.world_begin;
+  t.ret = kNoRet;
+  t.best = in.tmax0;
+  t.prim = kRefNone;
+  t.hit_ret = kNoRet;
+}
+
+// The current record is an NF box: test it (culling at best * (1 + 2^-10));
+// hit: the near child next, the far one pushed; miss: the stack's next.
+template <bool COUNT>
+MRT_DEV void trav_box_index_nf(const TravIn& in, const NfStack& k, Trav& t, LocalCounters& lc) {
+  if (COUNT) lc.node_visits++;
+  V3 mn{u2f(t.s0.x), u2f(t.s0.y), u2f(t.s0.z)}, mx{u2f(t.s0.w), u2f(t.s1.x), u2f(t.s1.y)};
+  if (box_hit_any<COUNT>(mn, mx, t.r, in.tmin, nf_cull(t.best), &lc)) {
+    const uint32_t w = t.s1.w, left = w & kNfIdx, axis = (w >> 28) & 3u;
+    if (axis == kNfLeaf) {
+      t.i = left;
+      return;
+    }
+    const float dk = axis == 0 ? t.r.d.x : (axis == 1 ? t.r.d.y : t.r.d.z);
+    const bool l_near = !(dk < 0.0f);
+    nf_push(k, t, l_near ? t.s1.z : left);
+    t.i = l_near ? left : t.s1.z;
+  } else if (!nf_pop(in, k, t)) {
+    nf_over(t);
+  }
+}
+
+// The current record is an NF leaf's primitive, instance or model.
+template <bool COUNT, uint32_t ALPHA>
+MRT_DEV void trav_prim_index_nf(const TravIn& in, const NfStack& k, Trav& t, LocalCounters& lc) {
+  const DevScene& S = in.S;
+  const uint4 s0 = t.s0, s1 = t.s1;
+  const uint32_t kind = s1.w;
+  uint32_t next;
+  if (kind == KIND_TRI) {
+    if (COUNT) lc.triangle_tests++;
+    const uint4 s2 = rec_load1<false>(in, t.i + 2);
+    V3 a{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, ab{u2f(s0.w), u2f(s1.x), u2f(s1.y)}, ac{u2f(s2.x), u2f(s2.y), u2f(s2.z)};
+    float th;
+    // tested up to the culling bound: hits beyond `best` are recorded in t2
+    if (tri_hit(a, ab, ac, t.r.o, t.r.d, in.tmin, nf_cull(t.best), th)) {
+      const uint32_t id = s1.z & kTriIdMask;
+      if (!ALPHA || !(s1.z & kTriAlpha) || tri_alpha_pass<false, ALPHA == 2>(S, id, t.r.o, t.r.d, th, t.rng, lc))
+        nf_hit(in, t, th, make_ref(MRT_REF_TRIANGLE, id));
+    }
+    next = s2.w;
+  } else if (kind == KIND_SPHERE) {
+    if (COUNT) lc.sphere_tests++;
+    float th;
+    if (sphere_hit(V3{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, u2f(s0.w), t.r.o, t.r.d, t.r.a, in.tmin, nf_cull(t.best), th))
+      nf_hit(in, t, th, make_ref(MRT_REF_SPHERE, s1.x));
+    next = s1.y;
+  } else {  // KIND_INST / KIND_MODEL: enter its BLAS, come back to the leaf's next record
+    if (s0.z != kNfPop) nf_push(k, t, s0.z);
+    nf_push(k, t, kNfRet);
+    if (kind == KIND_INST) {
+      if (COUNT) lc.instance_entries++;
+      V3 c0, c1, c2, c3;
+      load_m12(S.inst_inv + (size_t)MRT_IDX(S, s0.x, S.n_inst, 8) * 12, c0, c1, c2, c3);
+      t.r = make_tray(xform(c0, c1, c2, c3, t.r.o, 1.0f), xform(c0, c1, c2, c3, t.r.d, 0.0f), S.fast_ok);
+      t.ret = (t.i + 2) | kRetInstance;
+    } else {
+      if (COUNT) lc.model_entries++;
+      t.ret = t.i + 2;
+    }
+    t.i = s0.y;
+    return;
+  }
+  if (next != kNfPop) {
+    t.i = next;
+  } else if (!nf_pop(in, k, t)) {
+    nf_over(t);
+  }
 }
 
 // Whole traversal of pool ray `ray` (one ray per thread); RNG: the

@@ -132,11 +132,12 @@ __device__ __forceinline__ uint32_t wg_reserve(uint32_t* counter, uint32_t count
 
 __device__ void flush_counters(DevCounters* c, const LocalCounters& lc, uint32_t segs, uint32_t hits,
                                uint32_t samples, uint32_t bounces, uint32_t shaded = 0) {
-  uint32_t v[14] = {samples, segs, lc.node_visits, lc.sphere_tests, lc.triangle_tests, lc.instance_entries,
-                    lc.model_entries, hits, lc.texel_taps, bounces, lc.wave_slots, lc.lane_steps, lc.box_exact, shaded};
+  uint32_t v[15] = {samples, segs, lc.node_visits, lc.sphere_tests, lc.triangle_tests, lc.instance_entries,
+                    lc.model_entries, hits, lc.texel_taps, bounces, lc.wave_slots, lc.lane_steps, lc.box_exact, shaded,
+                    lc.vnf_fallbacks};
   unsigned long long* dst = reinterpret_cast<unsigned long long*>(c);
 #pragma unroll
-  for (int k = 0; k < 14; ++k) {
+  for (int k = 0; k < 15; ++k) {
     uint32_t s = wave_sum(v[k]);
     if (lane_id() == 0 && s) atomicAdd(dst + k, (unsigned long long)s);
   }
@@ -260,9 +261,14 @@ constexpr uint32_t kIdle = 0xFFFFFFFFu;  // Trav.ray of a lane without a ray
 // each ray carries its path stream through the traversal and stores it back.
 // (R > 1 would interleave R rays per lane — software ILP; measured slower at
 // its 84 VGPRs, so only R = 1 is instantiated.)
-template <bool COUNT, bool LDS, uint32_t ALPHA, bool RNG, int BLK>
-__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(ALPHA == 0 && !RNG && !COUNT ? 8 : 1))) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
+// NF: the verified near-first walk (path.h trav_*_nf): the SAH trees walked
+// near child first with a per-lane stack in LDS (kNfStack x BLK words of
+// dynamic shared memory), the winner checked against the reference tree,
+// rays that fail the check walked again the reference's way.
+template <bool COUNT, bool LDS, uint32_t ALPHA, bool RNG, int BLK, bool NF = false>
+__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(NF ? (COUNT ? 1 : 6) : (ALPHA == 0 && !RNG && !COUNT ? 8 : 1)))) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   DevCounters* cnt, float tmin, float tmax, TraceTune tune) {
+  static_assert(!NF || (!LDS && !RNG), "the near-first walk has no treelet and no traversal draws");
   constexpr int R = 1;
   const uint32_t n = ctrl->active[cur];
   if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = 0;
@@ -272,7 +278,8 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(ALPHA == 0 
     __syncthreads();
   }
   const TravIn tin{S, reinterpret_cast<const uint4*>(LDS ? S.slots_tl : S.slots), LDS ? S.tl_world_begin : S.world_begin,
-                   in.ro, in.rd, tmin, in.rng};
+                   in.ro, in.rd, tmin, in.rng, tmax};
+  const NfStack stk{reinterpret_cast<uint32_t*>(mrt_lds) + threadIdx.x, (uint32_t)BLK};
   LocalCounters lc;
   uint32_t seg = 0, nh = 0;
   uint32_t pool = 0, pool_end = 0;  // wave-uniform chunk [pool, pool_end)
@@ -319,7 +326,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(ALPHA == 0 
       for (int q = 0; q < R; ++q) {
         if (t[q].ray == kIdle) {
           const uint32_t r = off + lane_rank(idle[q]);
-          if (r < avail) trav_init<RNG, LDS>(tin, t[q], MRT_IDX(S, pool + r, n, 20), tmax);
+          if (r < avail) trav_init<RNG, LDS>(tin, t[q], MRT_IDX(S, pool + r, n, 20), tmax, NF ? S.nf_world : 0xFFFFFFFFu);
         }
         off += (uint32_t)__popcll(idle[q]);
         live |= __ballot(t[q].ray != kIdle);
@@ -342,8 +349,13 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(ALPHA == 0 
         const bool run_box = trav_at_box(t[q]);
         const unsigned long long bm = __builtin_amdgcn_ballot_w64(run_box);
         if ((uint32_t)__popcll(bm) < tune.box_min) return false;
-        if (run_box) trav_box_index<COUNT>(tin, t[q], lc);
-        if (run_box) trav_fetch<LDS>(tin, t[q]);
+        if (run_box) {
+          if (NF && t[q].sp != kExactMode)
+            trav_box_index_nf<COUNT>(tin, stk, t[q], lc);
+          else
+            trav_box_index<COUNT>(tin, t[q], lc);
+        }
+        if (run_box && (!NF || t[q].sp != kNfDone)) trav_fetch<LDS>(tin, t[q]);
         if (COUNT) {
           lc.wave_slots += lane_id() == 0 ? 64u : 0u;
           lc.lane_steps += run_box ? 1u : 0u;
@@ -352,14 +364,39 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(ALPHA == 0 
       };
       while (box_step() && box_step()) {
       }
-      const bool busy = !t[q].done;  // idle lanes hold a done Trav
+      // idle lanes hold a done Trav; a near-first lane whose walk is over
+      // waits for the check below
+      const bool busy = !t[q].done && (!NF || t[q].sp != kNfDone);
       const bool at_box = busy && trav_at_box(t[q]);
       const unsigned long long box_mask = __ballot(at_box);
       const unsigned long long prim_mask = __ballot(busy && !at_box);
-      if (at_box) trav_box<COUNT, LDS>(tin, t[q], lc);
+      if (at_box) {
+        if (NF && t[q].sp != kExactMode) {
+          trav_box_index_nf<COUNT>(tin, stk, t[q], lc);
+          if (t[q].sp != kNfDone) trav_fetch<LDS>(tin, t[q]);
+        } else {
+          trav_box<COUNT, LDS>(tin, t[q], lc);
+        }
+      }
       // primitives wait until enough lanes are at one (or no lane is at a box)
       const bool prim_go = (__popcll(prim_mask) >= tune.prim_batch || box_mask == 0) && busy && !at_box;
-      if (prim_go) trav_prim<COUNT, ALPHA, RNG, LDS>(tin, t[q], lc);
+      if (prim_go) {
+        if (NF && t[q].sp != kExactMode) {
+          trav_prim_index_nf<COUNT, ALPHA>(tin, stk, t[q], lc);
+          if (t[q].sp != kNfDone) trav_fetch<LDS>(tin, t[q]);
+        } else {
+          trav_prim<COUNT, ALPHA, RNG, LDS>(tin, t[q], lc);
+        }
+      }
+      // near-first walks that are over: check their hits (done, or the
+      // reference's walk from the start)
+      if (NF) {
+        const bool over = t[q].sp == kNfDone;
+        if (__builtin_amdgcn_ballot_w64(over) != 0 && over) {
+          nf_finish<COUNT>(tin, t[q], lc);
+          if (!t[q].done) trav_fetch<LDS>(tin, t[q]);
+        }
+      }
       if (COUNT) {
         lc.wave_slots += lane_id() == 0 ? 64u : 0u;
         lc.lane_steps += (at_box || prim_go) ? 1u : 0u;
@@ -945,6 +982,7 @@ enum OptId {
   OPT_TREELET_KB,        // LDS treelet per workgroup, KiB (0: none); applies at the next upload
   OPT_TRACE_BLOCK,       // k_trace workgroup size beside a treelet: 256, 512 or 1024
   OPT_MEM_RESERVE_MB,    // device memory a render leaves free when it sizes the pool and results slab
+  OPT_TRAVERSAL,         // 0: the reference's left-first walk; 1: the verified near-first walk (MRT_TRAVERSAL_*)
   kNumOpts
 };
 struct OptDef {
@@ -967,6 +1005,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"treelet_kb", 0, 0, 150},
     {"trace_block", 256, 256, 1024},
     {"mem_reserve_mb", 4096, 0, 1 << 20},
+    {"traversal", 0, 0, 1},
 };
 int opt_find(const char* name) {
   if (!name) return -1;
@@ -1048,6 +1087,9 @@ struct mrt_ctx {
   bool trace_lds = false;          // the scene has an LDS treelet (set per scene)
   int shade_wpe = 8;               // k_shade register budget: 8 or 7 waves/SIMD (option "shade_waves")
   uint32_t tl_boxes = 0;           // box records in the treelet
+  bool scene_nf = false;           // the scene has verified near-first trees (nf_tree.cpp)
+  std::string nf_note;             // why it has none
+  bool use_nf = false;             // k_trace walks them (option "traversal", the scene, no treelet)
   // LDS treelet: off by default. Measured: it removes the
   // global load of a step only when every lane of the wave is in the copy,
   // and the TA cost is per wave instruction, not per lane — 256/16 KB and
@@ -1167,6 +1209,7 @@ void apply_options(mrt_ctx* c) {
   c->treelet_kb = (uint32_t)o[OPT_TREELET_KB];
   c->trace_block = (int)o[OPT_TRACE_BLOCK];
   c->mem_reserve = (size_t)o[OPT_MEM_RESERVE_MB] << 20;
+  c->use_nf = o[OPT_TRAVERSAL] == MRT_TRAVERSAL_NEAR_FIRST && c->scene_nf && !c->trace_lds && !c->scene_rng;
   if (c->wgs_per_cu != (uint32_t)o[OPT_TRACE_WGS_PER_CU]) c->grids.clear();
   c->wgs_per_cu = (uint32_t)o[OPT_TRACE_WGS_PER_CU];
 }
@@ -1288,11 +1331,37 @@ void launch_trace_v(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& 
     launch_trace_r<LDS, ALPHA, false>(c, st, q, in, cur, count, tmin, tmax);
 }
 
+// The verified near-first walk (option "traversal" 1; scenes with NF trees,
+// no treelet, no traversal draws): its stack takes kNfStack words of LDS per lane.
+template <uint32_t ALPHA>
+void launch_trace_nf(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
+                     float tmin, float tmax) {
+  const size_t smem = (size_t)kNfStack * kBlock * 4;
+  const void* f = count ? (const void*)k_trace<true, false, ALPHA, false, kBlock, true>
+                        : (const void*)k_trace<false, false, ALPHA, false, kBlock, true>;
+  // the stack's LDS already bounds the grid below the VGPR occupancy: the
+  // other queue's kernels find wave slots beside it without the 3/4 share
+  const uint32_t grid = persistent_grid(c, f, smem, false, kBlock);
+  if (count)
+    hipLaunchKernelGGL((k_trace<true, false, ALPHA, false, kBlock, true>), dim3(grid), dim3(kBlock), smem, st, c->S, in,
+                       q.hits, q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
+  else
+    hipLaunchKernelGGL((k_trace<false, false, ALPHA, false, kBlock, true>), dim3(grid), dim3(kBlock), smem, st, c->S, in,
+                       q.hits, q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
+}
+
 void launch_trace(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
                   float tmin, float tmax) {
   // alpha tests: none / plain surfaces / composite surfaces (EXT)
   const uint32_t alpha = c->scene_alpha ? (c->scene_ext ? 2u : 1u) : 0u;
-  if (c->trace_lds) {
+  if (c->use_nf) {
+    if (alpha == 2)
+      launch_trace_nf<2>(c, st, q, in, cur, count, tmin, tmax);
+    else if (alpha == 1)
+      launch_trace_nf<1>(c, st, q, in, cur, count, tmin, tmax);
+    else
+      launch_trace_nf<0>(c, st, q, in, cur, count, tmin, tmax);
+  } else if (c->trace_lds) {
     if (alpha == 2)
       launch_trace_v<true, 2>(c, st, q, in, cur, count, tmin, tmax);
     else if (alpha == 1)
@@ -1934,6 +2003,7 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     const size_t o_sops = sec(hs.surf_ops.size() * sizeof(GpuSurfOp));
     const size_t o_bgf = sec(hs.bg_faces.size() * sizeof(GpuSurfRef));
     const size_t o_bgm = sec(sizeof(hs.bg_m));
+    const size_t o_vnf = sec(hs.vnf_leaf.size() * 4);
     if (c->scene_mem) HIP_CHECK(hipFree(c->scene_mem));
     c->scene_mem = nullptr;
     c->has_scene = false;
@@ -1961,6 +2031,7 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     up(o_sops, hs.surf_ops.data(), hs.surf_ops.size() * sizeof(GpuSurfOp));
     up(o_bgf, hs.bg_faces.data(), hs.bg_faces.size() * sizeof(GpuSurfRef));
     up(o_bgm, hs.bg_m, sizeof(hs.bg_m));
+    up(o_vnf, hs.vnf_leaf.data(), hs.vnf_leaf.size() * 4);
     DevScene S{};
     S.slots = (const uint32_t*)(base + o_slots);
     S.slots_tl = (const uint32_t*)(base + o_stl);
@@ -1999,16 +2070,24 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     S.n_surf_ops = (uint32_t)hs.surf_ops.size();
     S.bg_faces = (const GpuSurfRef*)(base + o_bgf);
     S.bg_m = (const float*)(base + o_bgm);
+    S.nf_ok = hs.nf_ok ? 1u : 0u;
+    S.nf_world = hs.nf_world;
+    S.vnf_leaf = (const uint32_t*)(base + o_vnf);
+    for (int k = 0; k < 4; ++k) S.vnf_base[k] = hs.vnf_base[k];
+    S.n_vnf = (uint32_t)(hs.vnf_leaf.size() / 2);
     c->S = S;
     c->scene_bytes = off;
     c->trace_lds = S.n_tlet > 0;
-    c->scene_big = (size_t)S.n_slots * 16 > ((size_t)16 << 20);
+    // the reference stream's size decides the per-scene rules (the NF trees follow it)
+    c->scene_big = (size_t)hs.nf_first_slot * 16 > ((size_t)16 << 20);
     c->scene_instances = S.n_inst;
-    apply_options(c);  // the per-scene rules of the options left at -1
     c->tl_boxes = hs.tl_boxes;
     c->scene_alpha = hs.has_alpha;
     c->scene_rng = hs.trav_rng;
     c->scene_ext = !hs.surf_ops.empty() || hs.bg_kind == MRT_BG_CUBEMAP;
+    c->scene_nf = hs.nf_ok;
+    c->nf_note = hs.nf_ok ? "" : hs.nf_note;
+    apply_options(c);  // the per-scene rules of the options left at -1
     c->has_scene = true;
   });
 }
@@ -2058,6 +2137,7 @@ int mrt_get_tuning(mrt_ctx* c, mrt_tuning* out) {
     out->shade_waves = (uint32_t)c->shade_wpe;
     out->pool_paths = c->pool_paths;
     out->results_max = c->results_max;
+    out->traversal = c->use_nf ? MRT_TRAVERSAL_NEAR_FIRST : MRT_TRAVERSAL_REFERENCE;
   });
 }
 
@@ -2192,6 +2272,7 @@ int mrt_get_counters(mrt_ctx* c, mrt_counters* out) {
     out->lane_steps = h.lane_steps;
     out->box_exact = h.box_exact;
     out->shaded = h.shaded;
+    out->vnf_fallbacks = h.vnf_fallbacks;
   });
 }
 

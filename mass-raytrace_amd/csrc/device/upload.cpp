@@ -562,6 +562,7 @@ bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err, b
   }
   if (e.mix_alpha) s.trav_rng = true;
   if (sibling_layout) relayout(s);  // false: the plain preorder stream (tools/slab_check.cpp layout check)
+  if (!build_nf_trees(d, s, err)) return false;  // appended after the reference stream (layout.h)
   if (s.slots.size() / 4 >= kLdsTag) return (err = "scene too large (record stream >= 2^30 slots)", false);
   return true;
 }

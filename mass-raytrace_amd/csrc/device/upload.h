@@ -48,7 +48,20 @@ struct HostScene {
   uint32_t tl_world_begin = 0, tl_boxes = 0;
   // statistics
   uint32_t n_box_records = 0, n_prim_records = 0, max_depth = 0;
+  // verified near-first trees (nf_tree.cpp): appended to `slots` after the
+  // reference stream (not in rec_starts: the treelet and relayout never see them)
+  bool nf_ok = false;
+  uint32_t nf_world = 0, nf_boxes = 0, nf_stack_need = 0, nf_first_slot = 0;
+  std::vector<uint32_t> vnf_leaf;  // {parent, key} pairs
+  uint32_t vnf_base[4] = {0, 0, 0, 0};
+  std::string nf_note;  // why a scene has no NF trees
 };
+
+// Builds the verified near-first trees of a linearised scene (after
+// build_host_scene; layout.h). A scene whose traversal draws random numbers,
+// or whose trees would need more than kNfStack stack entries, gets none
+// (nf_ok false, nf_note says why). Returns false only on an internal error.
+bool build_nf_trees(const mrt_scene_desc& d, HostScene& s, std::string& err);
 
 // Validates the description and linearises it. Returns false with `err` set.
 // sibling_layout=false keeps every region in plain preorder (the layout

@@ -151,13 +151,14 @@ class MrtKernelStats(C.Structure):
 class MrtTuning(C.Structure):
     _fields_ = [("queues", C.c_uint32), ("trace_refill", C.c_uint32), ("trace_box_min", C.c_uint32),
                 ("trace_chunk", C.c_uint32), ("shade_waves", C.c_uint32), ("pool_paths", C.c_uint64),
-                ("results_max", C.c_uint64)]
+                ("results_max", C.c_uint64), ("traversal", C.c_uint32)]
 
     def as_dict(self) -> dict:
         return {f: int(getattr(self, f)) for f, _ in self._fields_}
 
 
 GATHER_AUTO, GATHER_PEER, GATHER_RCCL = 0, 1, 2
+TRAVERSAL_REFERENCE, TRAVERSAL_NEAR_FIRST = 0, 1
 
 
 def env_options(env=None) -> dict:
@@ -174,7 +175,7 @@ def env_options(env=None) -> dict:
 
 
 # scheduling counters of the persistent k_trace (no reference counterpart)
-SCHED_FIELDS = ["wave_slots", "lane_steps", "box_exact", "shaded"]
+SCHED_FIELDS = ["wave_slots", "lane_steps", "box_exact", "shaded", "vnf_fallbacks"]
 
 
 class MrtCounters(C.Structure):

@@ -36,3 +36,25 @@ def test_sibling_layout_mesh(slab_check, assets_dir):
     r = subprocess.run([str(slab_check), "mesh_ply", "20000", str(assets_dir), "layout"], capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0 and " 0 of 20000 rays differ" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("scene", ["cornell", "sphere_grid", "cube_field"])
+def test_near_first_walk_finds_the_reference_hits(slab_check, scene):
+    """The verified near-first walk (nf_tree.cpp's trees, path.h's steps,
+    restated by tools/slab_check.cpp walk_nf): on camera and bounce rays the
+    same closest hits as the reference's left-first walk — primitive,
+    container, t bits — with fewer box tests; the stack stays within kNfStack."""
+    r = subprocess.run([str(slab_check), scene, "30000", str(GOLDEN), "nf"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " nf: 0 of 30000 rays differ" in r.stdout, r.stdout
+    boxes = r.stdout.split("box tests ")[1].split(" per ray")[0].split(" vs ")
+    assert float(boxes[0]) < float(boxes[1]), r.stdout
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("scene", ["mesh_ply", "menger_l3"])
+def test_near_first_walk_mesh_and_menger(slab_check, assets_dir, scene):
+    r = subprocess.run([str(slab_check), scene, "20000", str(assets_dir), "nf"], capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0 and " nf: 0 of 20000 rays differ" in r.stdout, r.stdout + r.stderr

@@ -765,6 +765,22 @@ int main(int argc, char** argv) {
          argv[1], (unsigned long long)rays, sr.boxes / R, sn.boxes / R, (double)sr.boxes / std::max<uint64_t>(sn.boxes, 1),
          (unsigned long long)diff_nf, (unsigned long long)diff_key_only, mlog, sm.boxes / R,
          (double)sr.boxes / std::max<uint64_t>(sm.boxes, 1), (unsigned long long)fallback, (unsigned long long)diff_nfm);
+  {
+    auto depth = [](const SahTree& t) {
+      std::vector<std::pair<int32_t, int>> st{{0, 1}};
+      int m = 0;
+      while (!st.empty()) {
+        auto [n, dd] = st.back();
+        st.pop_back();
+        m = std::max(m, dd);
+        if (t.nodes[n].l >= 0) st.push_back({t.nodes[n].l, dd + 1}), st.push_back({t.nodes[n].r, dd + 1});
+      }
+      return m;
+    };
+    int bm = 0;
+    for (auto& t : Z.blas) bm = std::max(bm, depth(t));
+    printf("%-12s sah depth: tlas %d, deepest blas %d\n", argv[1], depth(Z.tlas), bm);
+  }
   printf("%-12s sah+nf %.1f boxes/ray (x%.2f vs ref), prims %.1f vs %.1f, %llu differ (no margin, no check)\n", argv[1],
          ss.boxes / R, (double)sr.boxes / std::max<uint64_t>(ss.boxes, 1), ss.prims / R, sr.prims / R,
          (unsigned long long)diff_sah);

@@ -181,6 +181,157 @@ Result walk_plain(const HostScene& s, V o, V d, Stats* st = nullptr) {
   return {prim, cont, best};
 }
 
+// The verified near-first walk (layout.h; path.h trav_*_nf, nf_finish)
+// restated on the host: the NF trees near child first with a stack, the
+// reference's tie rule by order keys, the reachability check of the winner
+// on the reference stream, the reference's walk where it fails.
+uint64_t nf_key(const HostScene& s, uint32_t prim, uint32_t ret) {
+  const uint32_t* w = s.slots.data();
+  const uint32_t kind = prim >> 28, id = prim & 0x0FFFFFFFu;
+  auto entry = [&](uint32_t base, uint32_t i, int word) { return s.vnf_leaf[2 * (size_t)(s.vnf_base[base] + i) + word]; };
+  if (kind == MRT_REF_SPHERE) return (uint64_t)entry(VNF_SPHERE, id, 1) << 32;
+  const uint32_t k = entry(VNF_TRI, id, 1);
+  if (k & kWorldKey) return (uint64_t)(k & ~kWorldKey) << 32;
+  const uint32_t cid = w[4 * (size_t)((ret & 0x7FFFFFFFu) - 2)];
+  return ((uint64_t)entry((ret & 0x80000000u) ? VNF_INST : VNF_MODEL, cid, 1) << 32) | k;
+}
+Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks) {
+  const uint32_t* w = s.slots.data();
+  const Ray wr = make_ray(o, d, s.early_ok);
+  Ray r = wr;
+  uint32_t i = s.nf_world, ret = ~0u, hit_ret = ~0u, prim = 0;
+  float best = INFINITY, t2 = INFINITY;
+  std::vector<uint32_t> stack;
+  auto cull = [&]() { return std::fma(fabsf(best), 0x1p-10f, best); };
+  auto pop = [&]() {
+    while (!stack.empty()) {
+      const uint32_t v = stack.back();
+      stack.pop_back();
+      if (v != 0x80000000u) {
+        i = v;
+        return true;
+      }
+      if (ret & 0x80000000u) r = wr;
+      ret = ~0u;
+    }
+    return false;
+  };
+  auto better = [&](float t, uint32_t pr) {
+    if (t < best) return true;
+    if (!(t == best)) return false;
+    if (prim == 0) return true;
+    return nf_key(s, pr, ret) > nf_key(s, prim, hit_ret);
+  };
+  auto hit = [&](float t, uint32_t pr) {
+    if (t <= best && better(t, pr)) {
+      t2 = fminf(t2, best);
+      best = t, prim = pr, hit_ret = ret;
+    } else {
+      t2 = fminf(t2, t);
+    }
+  };
+  for (;;) {
+    const uint32_t* a = w + 4 * (size_t)i;
+    const uint32_t k = a[7];
+    if (k & kBoxFlag) {
+      float mn[3] = {f(a[0]), f(a[1]), f(a[2])}, mx[3] = {f(a[3]), f(a[4]), f(a[5])};
+      if (st) st->boxes++;
+      if (box_exact(mn, mx, r, kTmin, cull())) {
+        const uint32_t left = k & kNfIdx, axis = (k >> 28) & 3u;
+        if (axis == kNfLeaf) {
+          i = left;
+          continue;
+        }
+        const float dk = axis == 0 ? r.d.x : (axis == 1 ? r.d.y : r.d.z);
+        const bool ln = !(dk < 0.0f);
+        stack.push_back(ln ? a[6] : left);
+        if (stack.size() > kNfStack) {
+          fprintf(stderr, "nf: stack overflow\n");
+          exit(3);
+        }
+        i = ln ? left : a[6];
+      } else if (!pop()) {
+        break;
+      }
+      continue;
+    }
+    uint32_t next;
+    if (k == KIND_TRI) {
+      float t;
+      const uint32_t pr = MRT_REF(MRT_REF_TRIANGLE, a[6] & kTriIdMask);
+      if (tri_hit({f(a[0]), f(a[1]), f(a[2])}, {f(a[3]), f(a[4]), f(a[5])}, {f(a[8]), f(a[9]), f(a[10])}, r.o, r.d,
+                  kTmin, cull(), t))
+        hit(t, pr);
+      next = a[11];
+    } else if (k == KIND_SPHERE) {
+      float t;
+      const uint32_t pr = MRT_REF(MRT_REF_SPHERE, a[4]);
+      if (sphere_hit({f(a[0]), f(a[1]), f(a[2])}, f(a[3]), r.o, r.d, kTmin, cull(), t)) hit(t, pr);
+      next = a[5];
+    } else if (k == KIND_INST || k == KIND_MODEL) {
+      if (a[2] != kNfPop) stack.push_back(a[2]);
+      stack.push_back(0x80000000u);
+      if (k == KIND_INST) {
+        const float* m = &s.inst_inv[12 * (size_t)a[0]];
+        r = make_ray(xf(m, wr.o, 1.0f), xf(m, wr.d, 0.0f), s.early_ok);
+        ret = (i + 2) | 0x80000000u;
+      } else {
+        ret = i + 2;
+      }
+      i = a[1];
+      continue;
+    } else {
+      fprintf(stderr, "nf: unsupported kind %u at %u\n", k, i);
+      exit(2);
+    }
+    if (next != kNfPop) {
+      i = next;
+    } else if (!pop()) {
+      break;
+    }
+  }
+  // the check: the winner's innermost reference ancestors pass at
+  // tau = min(t2, best * (1 + 2^-10)), a lower bound of the reference's t_max there
+  bool ok = true;
+  const float tau = fminf(t2, cull());
+  auto box_at = [&](uint32_t rec, const Ray& rr) {
+    const uint32_t* b = w + 4 * (size_t)rec;
+    float mn[3] = {f(b[0]), f(b[1]), f(b[2])}, mx[3] = {f(b[3]), f(b[4]), f(b[5])};
+    if (st) st->boxes++;
+    return box_exact(mn, mx, rr, kTmin, tau);
+  };
+  if (prim) {
+    const uint32_t kind = prim >> 28, id = prim & 0x0FFFFFFFu;
+    const uint32_t own = s.vnf_leaf[2 * (size_t)(s.vnf_base[kind == MRT_REF_SPHERE ? VNF_SPHERE : VNF_TRI] + id)];
+    if (hit_ret == ~0u) {
+      if (own != kNoParent) ok = box_at(own, wr);
+    } else {
+      const bool inst = (hit_ret & 0x80000000u) != 0;
+      const uint32_t cid = w[4 * (size_t)((hit_ret & 0x7FFFFFFFu) - 2)];
+      const uint32_t wpar = s.vnf_leaf[2 * (size_t)(s.vnf_base[inst ? VNF_INST : VNF_MODEL] + cid)];
+      if (wpar != kNoParent) ok = box_at(wpar, wr);
+      if (ok && own != kNoParent) {
+        Ray rr = wr;
+        if (inst) {
+          const float* m = &s.inst_inv[12 * (size_t)cid];
+          rr = make_ray(xf(m, wr.o, 1.0f), xf(m, wr.d, 0.0f), s.early_ok);
+        }
+        ok = box_at(own, rr);
+      }
+    }
+  }
+  if (ok) {
+    uint32_t cont = 0;
+    if (hit_ret != ~0u) {
+      const uint32_t rec = (hit_ret & 0x7FFFFFFFu) - 2;
+      cont = MRT_REF((hit_ret & 0x80000000u) ? MRT_REF_INSTANCE : MRT_REF_MODEL, w[4 * (size_t)rec]);
+    }
+    return {prim, cont, best};
+  }
+  ++*fallbacks;
+  return walk_plain(s, o, d, st);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -207,6 +358,15 @@ int main(int argc, char** argv) {
   // same closest hits, t bits included, after the same number of box tests
   HostScene dfs;
   const bool layout = argc > 4 && !strcmp(argv[4], "layout");
+  // `nf` mode: the verified near-first walk must find the reference's closest
+  // hits (primitive, container, t bits) on every ray
+  const bool nf = argc > 4 && !strcmp(argv[4], "nf");
+  if (nf && !s.nf_ok) {
+    printf("%-14s nf: no near-first trees (%s)\n", argv[1], s.nf_note.c_str());
+    return 0;
+  }
+  uint64_t nf_bad = 0, nf_fallbacks = 0;
+  Stats nf_st;
   if (layout) {
     if (!build_host_scene(d, dfs, err, false)) return 1;
   }
@@ -236,6 +396,17 @@ int main(int argc, char** argv) {
     const uint64_t boxes0 = st.boxes;
     const Result r = walk_plain(s, ro, rd, &st);
     hits += r.prim != 0;
+    if (nf) {
+      const Result q = walk_nf(s, ro, rd, &nf_st, &nf_fallbacks);
+      uint32_t tb, qb;
+      memcpy(&tb, &r.t, 4);
+      memcpy(&qb, &q.t, 4);
+      const bool bad = r.prim != q.prim || r.container != q.container || (r.prim && tb != qb);
+      if (bad && nf_bad < 5)
+        fprintf(stderr, "nf differs: ref prim %08x cont %08x t %a | nf prim %08x cont %08x t %a\n", r.prim, r.container,
+                r.t, q.prim, q.container, q.t);
+      nf_bad += bad;
+    }
     if (layout) {
       Stats sd;
       const Result q = walk_plain(dfs, ro, rd, &sd);
@@ -244,6 +415,14 @@ int main(int argc, char** argv) {
       memcpy(&qb, &q.t, 4);
       layout_bad += r.prim != q.prim || r.container != q.container || tb != qb || sd.boxes != st.boxes - boxes0;
     }
+  }
+  if (nf) {
+    printf("%-14s nf: %llu of %d rays differ from the reference walk; box tests %.1f vs %.1f per ray (x%.2f), "
+           "%llu fallbacks (%.2f%%), stack need %u\n",
+           argv[1], (unsigned long long)nf_bad, n, (double)nf_st.boxes / n, (double)st.boxes / n,
+           (double)st.boxes / std::max<uint64_t>(nf_st.boxes, 1), (unsigned long long)nf_fallbacks,
+           100.0 * nf_fallbacks / n, s.nf_stack_need);
+    if (nf_bad) return 1;
   }
   if (layout) {
     printf("%-14s layout: %llu of %d rays differ between the sibling layout and the preorder stream; stream %zu vs %zu slots\n",
