@@ -218,9 +218,11 @@ def test_constrained_memory_renders_in_chunks(scene):
     one = _ctx(scene)
     ref = one.render(Wl, Hl, 0, spp, seed=12)
     one.close()
-    free_mb = torch.cuda.mem_get_info(0)[0] >> 20
-    multi = massrt.Context(devices=[0, 0, 0], options={"mem_reserve_mb": max(0, free_mb - 300)})
+    multi = massrt.Context(devices=[0, 0, 0])
     multi.upload(scene)
+    multi.render(Wl, Hl, 0, 1, seed=12)  # the per-frame buffers, kernels and scratch in place at 1 spp
+    free_mb = torch.cuda.mem_get_info(0)[0] >> 20  # what the 24-spp render re-plans its pools and slabs from
+    multi.set_option("mem_reserve_mb", max(0, free_mb - 400))
     got = multi.render(Wl, Hl, 0, spp, seed=12)
     t = multi.tuning()
     multi.close()
