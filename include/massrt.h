@@ -337,9 +337,11 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  *   trace_block       256, 512, 1024  k_trace workgroup beside a treelet
  *   mem_reserve_mb    device memory a render leaves free (default 4096)
  *   gather            MRT_GATHER_* (multi-device contexts)
- *   traversal         MRT_TRAVERSAL_* (default REFERENCE); NEAR_FIRST applies
+ *   traversal         MRT_TRAVERSAL_* (default NEAR_FIRST); NEAR_FIRST applies
  *                     to scenes without traversal draws (Volume, Mix alpha)
  *                     and without a treelet, others keep REFERENCE
+ *   trace_nf_batch    -1, 1..64  NEAR_FIRST: finished walks checked together
+ *                     once this many lanes wait (-1: the refill threshold)
  * Every render sizes its path pool and results slab to the device memory
  * free at that moment minus mem_reserve_mb (several contexts may share a
  * device), shrinking the pool first and then the samples per chunk. */
@@ -350,7 +352,8 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  * that the reference's walk reaches the hit it found (its innermost reference
  * ancestors pass BoundingBox::hit at that t) and walks the reference's way
  * where it does not — the same closest hits, ties included, from fewer box
- * tests. Counters (node visits, ...) then count its work. */
+ * tests. Counters (node visits, ...) then count its work;
+ * set REFERENCE for the reference's own traversal counts. */
 #define MRT_TRAVERSAL_REFERENCE 0
 #define MRT_TRAVERSAL_NEAR_FIRST 1
 #define MRT_GATHER_AUTO 0 /* RCCL between distinct devices, peer copies otherwise */

@@ -247,6 +247,7 @@ struct TraceTune {
   uint32_t prim_batch = 1;   // run the primitive branch once this many lanes wait at one
   uint32_t box_min = 24;     // inner box loop while this many lanes are at a box (65: off)
   uint32_t shade_batch = 16; // k_render: shade once this many lanes finished a segment
+  uint32_t nf_batch = 32;    // near-first walk: check the hits once this many lanes' walks are over
 };
 
 // LDS=true: the scene's treelet (layout.h, upload.cpp build_treelet) is first
@@ -389,10 +390,15 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(NF ? (COUNT
         }
       }
       // near-first walks that are over: check their hits (done, or the
-      // reference's walk from the start)
+      // reference's walk from the start) — batched: the check is a few
+      // hundred wave instructions, so finished lanes wait (holding an END
+      // record) until tune.nf_batch of them can share one pass, or until no
+      // lane is walking any more
       if (NF) {
         const bool over = t[q].sp == kNfDone;
-        if (__builtin_amdgcn_ballot_w64(over) != 0 && over) {
+        const unsigned long long om = __builtin_amdgcn_ballot_w64(over);
+        if (om != 0 && ((uint32_t)__popcll(om) >= tune.nf_batch ||
+                        __builtin_amdgcn_ballot_w64(!t[q].done && !over) == 0) && over) {
           nf_finish<COUNT>(tin, t[q], lc);
           if (!t[q].done) trav_fetch<LDS>(tin, t[q]);
         }
@@ -983,6 +989,7 @@ enum OptId {
   OPT_TRACE_BLOCK,       // k_trace workgroup size beside a treelet: 256, 512 or 1024
   OPT_MEM_RESERVE_MB,    // device memory a render leaves free when it sizes the pool and results slab
   OPT_TRAVERSAL,         // 0: the reference's left-first walk; 1: the verified near-first walk (MRT_TRAVERSAL_*)
+  OPT_TRACE_NF_BATCH,    // near-first walk: lanes whose walks are over wait for this many to check their hits together (-1: = refill)
   kNumOpts
 };
 struct OptDef {
@@ -1005,7 +1012,8 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"treelet_kb", 0, 0, 150},
     {"trace_block", 256, 256, 1024},
     {"mem_reserve_mb", 4096, 0, 1 << 20},
-    {"traversal", 0, 0, 1},
+    {"traversal", 1, 0, 1},
+    {"trace_nf_batch", -1, -1, 64},
 };
 int opt_find(const char* name) {
   if (!name) return -1;
@@ -1204,6 +1212,7 @@ void apply_options(mrt_ctx* c) {
                                               : (inst ? 16u : (big ? 32u : 24u));
   c->tune.chunk = o[OPT_TRACE_CHUNK] >= 0 ? (uint32_t)o[OPT_TRACE_CHUNK] : ((big || inst) ? 128u : 512u);
   c->tune.prim_batch = (uint32_t)o[OPT_TRACE_PRIM_BATCH];
+  c->tune.nf_batch = o[OPT_TRACE_NF_BATCH] > 0 ? (uint32_t)o[OPT_TRACE_NF_BATCH] : c->tune.refill;
   c->tune.shade_batch = (uint32_t)o[OPT_SHADE_BATCH];
   c->shade_wpe = o[OPT_SHADE_WAVES] >= 0 ? (int)o[OPT_SHADE_WAVES] : ((big && !inst) ? 7 : 8);
   c->treelet_kb = (uint32_t)o[OPT_TREELET_KB];
@@ -1224,6 +1233,7 @@ void set_option(mrt_ctx* c, int id, int64_t v) {
     throw ApiError{MRT_ERR_INVALID, "option trace_block must be 256, 512 or 1024"};
   if (id == OPT_SHADE_WAVES && v != -1 && v != 7 && v != 8)
     throw ApiError{MRT_ERR_INVALID, "option shade_waves must be 7, 8 or -1 (per scene)"};
+  if (id == OPT_TRACE_NF_BATCH && v == 0) throw ApiError{MRT_ERR_INVALID, "option trace_nf_batch must be 1..64 or -1"};
   if (id == OPT_TRACE_CHUNK && v != -1 && v < 64) throw ApiError{MRT_ERR_INVALID, "option trace_chunk must be >= 64 or -1"};
   if (id == OPT_QUEUES && v != c->opt[id] && c->pool_mem) {  // the pool is split per queue: reallocated at the next render
     HIP_CHECK(hipDeviceSynchronize());
@@ -1339,9 +1349,10 @@ void launch_trace_nf(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs&
   const size_t smem = (size_t)kNfStack * kBlock * 4;
   const void* f = count ? (const void*)k_trace<true, false, ALPHA, false, kBlock, true>
                         : (const void*)k_trace<false, false, ALPHA, false, kBlock, true>;
-  // the stack's LDS already bounds the grid below the VGPR occupancy: the
-  // other queue's kernels find wave slots beside it without the 3/4 share
-  const uint32_t grid = persistent_grid(c, f, smem, false, kBlock);
+  // 80 VGPRs and kNfStack KiB of LDS per workgroup both allow 6 waves per
+  // SIMD: a full grid leaves the other queue's k_shade no VGPRs, so the walk
+  // takes the 3/4 share like the reference walk's grid
+  const uint32_t grid = persistent_grid(c, f, smem, c->n_queues > 1, kBlock);
   if (count)
     hipLaunchKernelGGL((k_trace<true, false, ALPHA, false, kBlock, true>), dim3(grid), dim3(kBlock), smem, st, c->S, in,
                        q.hits, q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);

@@ -49,9 +49,29 @@ def assets_dir():
     return ensure_assets(REPO / "assets", mesh=True, textures=True, environment=True)
 
 
-@pytest.fixture(scope="session")
-def ctx():
+@pytest.fixture(scope="session", params=["reference", "near_first"])
+def ctx(request):
+    """A context per walk (option traversal): every test that takes `ctx`
+    runs on the reference's left-first walk and on the near-first walk."""
     import massrt
-    c = massrt.Context(0)  # raises loudly without a GPU: there is no fallback
+    walk = massrt.TRAVERSAL_REFERENCE if request.param == "reference" else massrt.TRAVERSAL_NEAR_FIRST
+    c = massrt.Context(0, options={"traversal": walk})  # raises loudly without a GPU: there is no fallback
     yield c
     c.close()
+
+
+# counters of the walk itself: the near-first walk does other work for the
+# same hits (tests/test_gpu_nearfirst.py); the rest must match either way
+WALK_COUNTERS = {"node_visits", "sphere_tests", "triangle_tests", "instance_entries", "model_entries", "box_exact",
+                 "wave_slots", "lane_steps", "vnf_fallbacks", "alpha_taps",
+                 "texel_taps"}  # texel taps: alpha tests during the walk sample textures too
+
+
+def walk_keys(c, keys):
+    """`keys` to compare with the oracle's counters for context c's current
+    scene: all of them on the reference's walk, the walk-independent ones on
+    the near-first walk."""
+    import massrt
+    if c.tuning()["traversal"] == massrt.TRAVERSAL_REFERENCE:
+        return list(keys)
+    return [k for k in keys if k not in WALK_COUNTERS]

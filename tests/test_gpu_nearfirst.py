@@ -57,7 +57,7 @@ def test_render_equals_the_reference_walk(nf_ctx, small, golden_dir, scene):
     """Same samples, both walks: bit-identical sums and bounce counts; and
     against the oracle as the other parity tests do."""
     b, o = small[scene]
-    ref = massrt.Context(0)
+    ref = massrt.Context(0, options={"traversal": massrt.TRAVERSAL_REFERENCE})
     ref.upload(b)
     nf_ctx.upload(b)
     W, H, spp = 160, 90, 4
