@@ -553,6 +553,9 @@ def roofline_for(a, scene, cnt, ks, samples_total, elapsed, n_gpus, plan) -> tup
         "lane_utilisation": round(cnt["lane_steps"] / max(cnt["wave_slots"], 1), 4),
         # box tests the early slab decision left to the exact test (path.h box_hit_any)
         "box_exact_frac": round(cnt.get("box_exact", 0) / max(cnt["node_visits"], 1), 5),
+        # near-first walk (option traversal=1): segments whose hit check sent
+        # them back to the reference's walk (path.h nf_finish)
+        "vnf_fallback_frac": round(cnt.get("vnf_fallbacks", 0) / max(cnt["segments"], 1), 6),
     }
     shade = None
     if cnt.get("shaded") and ks["shade_launches"] > 0:

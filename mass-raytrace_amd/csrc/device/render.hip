@@ -1199,26 +1199,34 @@ void set_device(mrt_ctx* c) { HIP_CHECK(hipSetDevice(c->device)); }
 //    its waves end on longer tails);
 //  * k_shade at 7 waves/SIMD for a big non-instanced world (mesh_ply 948.6
 //    -> 969.0), else 8 (sphere_grid 808.8, 7: 778.1; profiles/r3_tune2/wpe.txt).
+//  The near-first walk (round 4, profiles/r4_nf/tune.txt) has rules of its
+//  own: refill 24 and box run >= 28 lanes for a big non-instanced world
+//  (mesh_ply 1383.7 -> 1432.6), 512 rays per grab except there (cube_field
+//  556.2 -> 580.2 with shade 7; mesh_ply keeps 128: 1386.7 vs 1372.7), and
+//  k_shade at 7 waves/SIMD everywhere (sphere_grid 983.3 -> 992.9).
 void apply_options(mrt_ctx* c) {
   const int64_t* o = c->opt;
   const bool inst = c->scene_instances > 1000, big = c->scene_big;
+  c->treelet_kb = (uint32_t)o[OPT_TREELET_KB];
+  c->use_nf = o[OPT_TRAVERSAL] == MRT_TRAVERSAL_NEAR_FIRST && c->scene_nf && !c->trace_lds && !c->scene_rng;
+  const bool nf = c->use_nf, big_solid = big && !inst;
   c->n_queues = (int)o[OPT_QUEUES];
   c->pool_paths = (size_t)o[OPT_POOL_PATHS];
   c->results_max = 1ull << o[OPT_RESULTS_LOG2];
   c->finish_paths = (uint32_t)o[OPT_FINISH_PATHS];
   c->finish_grid_div = (uint32_t)o[OPT_FINISH_GRID_DIV];
-  c->tune.refill = o[OPT_TRACE_REFILL] >= 0 ? (uint32_t)std::max<int64_t>(1, o[OPT_TRACE_REFILL]) : 32u;
+  c->tune.refill = o[OPT_TRACE_REFILL] >= 0 ? (uint32_t)std::max<int64_t>(1, o[OPT_TRACE_REFILL])
+                                            : ((nf && big_solid) ? 24u : 32u);
   c->tune.box_min = o[OPT_TRACE_BOX_MIN] >= 0 ? (uint32_t)std::max<int64_t>(1, o[OPT_TRACE_BOX_MIN])
-                                              : (inst ? 16u : (big ? 32u : 24u));
-  c->tune.chunk = o[OPT_TRACE_CHUNK] >= 0 ? (uint32_t)o[OPT_TRACE_CHUNK] : ((big || inst) ? 128u : 512u);
+                                              : (inst ? 16u : (big ? (nf ? 28u : 32u) : 24u));
+  c->tune.chunk = o[OPT_TRACE_CHUNK] >= 0 ? (uint32_t)o[OPT_TRACE_CHUNK]
+                                          : (nf ? (big_solid ? 128u : 512u) : ((big || inst) ? 128u : 512u));
   c->tune.prim_batch = (uint32_t)o[OPT_TRACE_PRIM_BATCH];
   c->tune.nf_batch = o[OPT_TRACE_NF_BATCH] > 0 ? (uint32_t)o[OPT_TRACE_NF_BATCH] : c->tune.refill;
   c->tune.shade_batch = (uint32_t)o[OPT_SHADE_BATCH];
-  c->shade_wpe = o[OPT_SHADE_WAVES] >= 0 ? (int)o[OPT_SHADE_WAVES] : ((big && !inst) ? 7 : 8);
-  c->treelet_kb = (uint32_t)o[OPT_TREELET_KB];
+  c->shade_wpe = o[OPT_SHADE_WAVES] >= 0 ? (int)o[OPT_SHADE_WAVES] : ((nf || big_solid) ? 7 : 8);
   c->trace_block = (int)o[OPT_TRACE_BLOCK];
   c->mem_reserve = (size_t)o[OPT_MEM_RESERVE_MB] << 20;
-  c->use_nf = o[OPT_TRAVERSAL] == MRT_TRAVERSAL_NEAR_FIRST && c->scene_nf && !c->trace_lds && !c->scene_rng;
   if (c->wgs_per_cu != (uint32_t)o[OPT_TRACE_WGS_PER_CU]) c->grids.clear();
   c->wgs_per_cu = (uint32_t)o[OPT_TRACE_WGS_PER_CU];
 }
