@@ -10,7 +10,8 @@ SCENE=${SCENE:-sphere_grid}
 TAG=${TAG:-}   # e.g. TAG=_solo with MASSRT_OPTIONS=queues=1: profiles/pmc_<scene>_solo.json
 OUT=gpurun_out/prof_$SCENE$TAG
 rm -rf $OUT; mkdir -p $OUT
-B="bench.py --scene $SCENE --no-cpu-baseline --no-dropin --no-configs --secondary none"
+# BENCH_EXTRA: the config's own size, e.g. "--width 3840 --height 2160 --spp-per-step 256" (config 5)
+B="bench.py --scene $SCENE --no-cpu-baseline --no-dropin --no-configs --secondary none $BENCH_EXTRA"
 P="--steps 1 --warmup 1 --no-kernel-timing"
 run() {  # name, timeout, rocprofv3 args...
   local name=$1 t=$2; shift 2
