@@ -56,22 +56,31 @@ constexpr uint32_t kTriIdMask = 0x0FFFFFFFu;
 // A second set of trees over the same primitives, appended to the slot
 // array after the reference stream: a surface-area-heuristic BVH over the
 // world's objects (spheres, instances, models, world triangles) and one per
-// BLAS, walked near child first with a per-lane stack (k_trace's NF variant).
+// BLAS, walked nearer child first (by entry distance) with a per-lane stack
+// (k_trace's NF variant).
 // The walk finds the closest hit with the reference's tie rule (the later
 // primitive in the reference's left-first order wins, keys below), then the
 // winner is checked against the REFERENCE tree (its two innermost reference
 // ancestors must pass BoundingBox::hit at the winning t — nested boxes, so the
 // outer ones do too — i.e. the reference's left-first walk reaches it); a ray
 // that fails the check is traced again the reference's way.
-//   NF BOX  2 slots {min.x,min.y,min.z,max.x} {max.y,max.z,right,kBoxFlag|axis<<28|left}
-//           axis 0..2: the near child is left when d[axis] >= 0, else right;
-//           axis 3 (kNfLeaf): a leaf, `left` = its first primitive record
+//   NF NODE 2 slots {o.x,o.y,o.z,ex|ey<<8|ez<<16|lsz<<24} {qa,qb,qc,kBoxFlag|base}
+//           an inner node holding BOTH children's boxes, each plane 8 bits in
+//           the node's frame: plane = o.k + q * 2^(e.k - 127) (real value;
+//           lo planes rounded down, hi planes up — conservative, which is all
+//           the walk needs: its hits are checked against the reference tree,
+//           never its boxes). q bytes, low first: qa = {L.lo.x, L.lo.y, L.lo.z,
+//           L.hi.x}, qb = {L.hi.y, L.hi.z, R.lo.x, R.lo.y}, qc = {R.lo.z,
+//           R.hi.x, R.hi.y, R.hi.z}. The children are the records at `base`
+//           (left, lsz slots) and base + lsz (right): a node, or a leaf's first
+//           primitive. One 32-B record decides two boxes (the reference
+//           stream's box record decides one): half the vector loads per box.
 //   SPHERE / TRI as in the reference stream, `next` = the leaf's following
 //           record or kNfPop (continue with the stack)
 //   INST / MODEL {id, nf_blas_root, next, 0} {0,0,0,INST|MODEL}
-constexpr uint32_t kNfIdx = 0x0FFFFFFFu;  // index bits of an NF box's left child
+constexpr uint32_t kNfIdx = 0x0FFFFFFFu;  // index bits of an NF node's children base
 constexpr uint32_t kNfPop = 0x0FFFFFFFu;  // "next" of a leaf's last record: pop the stack
-constexpr uint32_t kNfLeaf = 3u;           // axis field of a leaf box
+constexpr int kNfExpMin = -100;            // smallest plane step 2^e (products with 1/d stay normal)
 constexpr uint32_t kNfStack = 24u;         // stack entries per lane (LDS): the trees' depth is capped to fit
 constexpr uint32_t kNoParent = 0xFFFFFFFFu;
 // Verification record of a leaf object (DevScene::vnf_leaf[vnf_base[kind] + id]):

@@ -12,6 +12,7 @@
 // primitive of its order — which a near-first walk of any tree finds — and
 // whether it reaches it is a property of the winner's ancestor boxes alone.
 #include <math.h>
+#include <cmath>
 #include <string.h>
 
 #include <algorithm>
@@ -93,7 +94,7 @@ struct Item {
 struct Node {
   Box b;
   int32_t l = -1, r = -1;
-  uint32_t first = 0, count = 0, axis = kNfLeaf;
+  uint32_t first = 0, count = 0, axis = 0;
 };
 struct Tree {
   std::vector<Node> nodes;
@@ -200,53 +201,97 @@ struct Builder {
     return i;
   }
 
-  // emits tree t depth-first (a box, its left subtree, its right subtree);
-  // returns the root record
-  uint32_t emit(const Tree& t) {
-    struct F {
-      int32_t node;
-      uint32_t patch;  // != ~0: the box record whose `right` is this subtree
-    };
-    std::vector<F> st{{0, ~0u}};
-    uint32_t root = ~0u;
-    while (!st.empty()) {
-      const F f = st.back();
-      st.pop_back();
-      const Node& n = t.nodes[f.node];
-      const uint32_t at = n_slots();
-      if (f.patch != ~0u) w[4 * (f.patch + 1) + 2] = at;
-      if (root == ~0u) root = at;
-      push(f2u(n.b.mn[0]), f2u(n.b.mn[1]), f2u(n.b.mn[2]), f2u(n.b.mx[0]));
-      push(f2u(n.b.mx[1]), f2u(n.b.mx[2]), 0, 0);
-      s.nf_boxes++;
-      for (int k = 0; k < 3; ++k) {
-        for (float v : {n.b.mn[k], n.b.mx[k]}) {
-          const float a = fabsf(v);
-          if (!(a == 0.0f || (a >= 0x1p-40f && a <= 0x1p28f))) s.fast_ok = 0;
-          if (!(a <= 0x1p28f)) s.early_ok = 0;
-        }
-      }
-      if (n.l < 0) {  // a leaf: its records follow the box
-        w[4 * (at + 1) + 3] = kBoxFlag | (kNfLeaf << 28) | (at + 2);
-        for (uint32_t k = 0; k < n.count; ++k) leaf_record(t.items[n.first + k].rec, k + 1 == n.count);
-      } else {
-        w[4 * (at + 1) + 3] = kBoxFlag | (n.axis << 28) | (at + 2);  // left: right after the box
-        st.push_back({n.r, at});
-        st.push_back({n.l, ~0u});
-      }
+  // Quantized frame of a node over its children's boxes a, b (layout.h NF
+  // NODE): origin = the union's min, per axis the smallest step 2^e with
+  // 254 steps covering the union (one step of slack for the rounding of the
+  // double arithmetic below, whose error is < 2^-40 of a step); planes rounded
+  // outward. false: a box is not finite (or past the exponent range).
+  static bool quantize(const Box& a, const Box& b, uint32_t o[3], uint32_t& ew, uint32_t q[3]) {
+    uint8_t bytes[12];
+    ew = 0;
+    for (int k = 0; k < 3; ++k) {
+      const float org = fminf(a.mn[k], b.mn[k]);
+      const double hi = std::max((double)a.mx[k], (double)b.mx[k]);
+      if (!(fabsf(org) < INFINITY) || !(fabs(hi) < INFINITY)) return false;
+      const double ext = hi - (double)org;
+      int e = kNfExpMin;
+      while (std::ldexp(254.0, e) < ext) ++e;
+      if (e > 127) return false;
+      const double step = std::ldexp(1.0, e);
+      auto lo_q = [&](float v) {
+        return (uint8_t)std::max(0.0, std::floor(((double)v - org) / step - 0x1p-30));
+      };
+      auto hi_q = [&](float v) {
+        return (uint8_t)std::min(255.0, std::ceil(((double)v - org) / step + 0x1p-30));
+      };
+      o[k] = f2u(org);
+      ew |= (uint32_t)(e + 127) << (8 * k);
+      bytes[k] = lo_q(a.mn[k]);
+      bytes[3 + k] = hi_q(a.mx[k]);
+      bytes[6 + k] = lo_q(b.mn[k]);
+      bytes[9 + k] = hi_q(b.mx[k]);
     }
-    return root;
+    for (int j = 0; j < 3; ++j)
+      q[j] = bytes[4 * j] | (uint32_t)bytes[4 * j + 1] << 8 | (uint32_t)bytes[4 * j + 2] << 16 |
+             (uint32_t)bytes[4 * j + 3] << 24;
+    return true;
   }
-  // copy of reference record `r` with the leaf's successor (kNfPop when last)
-  void leaf_record(uint32_t r, bool last) {
-    const uint32_t k = kind_of(w, r);
-    const uint32_t at = n_slots();
-    const uint32_t nslot = k == KIND_TRI ? 3 : 2;
-    const uint32_t next = last ? kNfPop : at + nslot;
-    for (uint32_t q = 0; q < 4 * nslot; ++q) {
-      const uint32_t v = w[4 * (size_t)r + q];  // (w may reallocate)
-      w.push_back(v);
+
+  uint32_t rec_slots(uint32_t r) const { return kind_of(w, r) == KIND_TRI ? 3u : 2u; }
+  // slots of the record a child of a node starts with (a node, or its leaf's first object)
+  uint32_t child_slots(const Tree& t, const Node& c) const { return c.l < 0 ? rec_slots(t.items[c.first].rec) : 2u; }
+
+  // writes leaf n's objects: the first at `at` (reserved), the rest appended
+  void emit_leaf(const Tree& t, const Node& n, uint32_t at) {
+    uint32_t pos = at;
+    for (uint32_t k = 0; k < n.count; ++k) {
+      const uint32_t r = t.items[n.first + k].rec;
+      if (k > 0) {
+        pos = n_slots();
+        for (uint32_t z = 0; z < 4 * rec_slots(r); ++z) w.push_back(0);
+      }
+      const uint32_t next = k + 1 == n.count ? kNfPop : std::max(n_slots(), pos + rec_slots(r));
+      copy_record(r, pos, next);
     }
+  }
+  // node n's record at `at` (reserved): its children's records follow as a
+  // pair, then their subtrees (left first)
+  bool emit_node(const Tree& t, const Node& n, uint32_t at) {
+    const Node& L = t.nodes[n.l];
+    const Node& R = t.nodes[n.r];
+    const uint32_t lsz = child_slots(t, L), rsz = child_slots(t, R), base = n_slots();
+    for (uint32_t z = 0; z < 4 * (lsz + rsz); ++z) w.push_back(0);
+    uint32_t o[3], ew, q[3];
+    if (!quantize(L.b, R.b, o, ew, q)) return false;
+    uint32_t* rec = &w[4 * (size_t)at];
+    rec[0] = o[0], rec[1] = o[1], rec[2] = o[2], rec[3] = ew | lsz << 24;
+    rec[4] = q[0], rec[5] = q[1], rec[6] = q[2], rec[7] = kBoxFlag | base;
+    s.nf_boxes++;
+    for (const auto& [c, pos] : {std::pair<const Node*, uint32_t>{&L, base}, {&R, base + lsz}}) {
+      if (c->l < 0)
+        emit_leaf(t, *c, pos);
+      else if (!emit_node(t, *c, pos))
+        return false;
+    }
+    return true;
+  }
+  // emits tree t; returns its root record (a node, or a leaf's first object),
+  // ~0u when a box cannot be quantized
+  uint32_t emit(const Tree& t) {
+    const Node& root = t.nodes[0];
+    const uint32_t at = n_slots();
+    const uint32_t sz = child_slots(t, root);
+    for (uint32_t z = 0; z < 4 * sz; ++z) w.push_back(0);
+    if (root.l < 0) {
+      emit_leaf(t, root, at);
+      return at;
+    }
+    return emit_node(t, root, at) ? at : ~0u;
+  }
+  // reference record `r` copied to slot `at` with the leaf's successor `next`
+  void copy_record(uint32_t r, uint32_t at, uint32_t next) {
+    const uint32_t k = kind_of(w, r);
+    for (uint32_t q = 0; q < 4 * rec_slots(r); ++q) w[4 * (size_t)at + q] = w[4 * (size_t)r + q];
     switch (k) {
       case KIND_TRI: w[4 * (at + 2) + 3] = next; break;
       case KIND_SPHERE: w[4 * (at + 1) + 1] = next; break;
@@ -397,8 +442,13 @@ struct Builder {
     s.nf_stack_need = world.depth + (has_blas ? 2 + blas_depth : 0);
     if (s.nf_stack_need > kNfStack) return (s.nf_note = "trees deeper than the walk's stack", true);
     s.nf_world = emit(world);
-    for (size_t k = 0; k < blas.size(); ++k)
-      if (!blas[k].items.empty()) blas_root[s.blas_regions[k].begin] = emit(blas[k]);
+    if (s.nf_world == ~0u) return (s.nf_note = "a box the node format cannot hold (not finite)", true);
+    for (size_t k = 0; k < blas.size(); ++k) {
+      if (blas[k].items.empty()) continue;
+      const uint32_t root = emit(blas[k]);
+      if (root == ~0u) return (s.nf_note = "a box the node format cannot hold (not finite)", true);
+      blas_root[s.blas_regions[k].begin] = root;
+    }
     for (auto& [rec, ref_blas] : patches) {
       auto it = blas_root.find(ref_blas);
       if (it == blas_root.end()) return (err = "NF: an instance of an empty BLAS", false);

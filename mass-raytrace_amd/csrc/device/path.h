@@ -824,22 +824,74 @@ MRT_DEV void nf_finish(const TravIn& in, Trav& t, LocalCounters& lc) {
   t.hit_ret = kNoRet;
 }
 
-// The current record is an NF box: test it (culling at best * (1 + 2^-10));
-// hit: the near child next, the far one pushed; miss: the stack's next.
+// Both children's boxes of an NF node (layout.h NF NODE) against [tmin,
+// tmax]: hit[c] unless the box is certainly missed, ent[c] its entry t. Fast
+// rays: plane t = q * (2^e * y) + (o * y - oy) — 2^e * y is exact, so the
+// error against (plane - o_ray) / d adds the node's |o * y - oy| term to the
+// early decision's margin (box_hit_any) — and only a certain miss counts as
+// one: the walk's boxes may be loose (its hits are checked against the
+// reference tree), never tight. Other rays: the exact test on the decoded
+// planes, each widened by an ulp.
+MRT_DEV void nf_node_test(const uint4& s0, const uint4& s1, const TRay& r, float tmin, float tmax, bool hit[2],
+                          float ent[2]) {
+  const V3 o{u2f(s0.x), u2f(s0.y), u2f(s0.z)};
+  const V3 sc{__uint_as_float((s0.w & 0xFFu) << 23), __uint_as_float(((s0.w >> 8) & 0xFFu) << 23),
+              __uint_as_float(((s0.w >> 16) & 0xFFu) << 23)};
+  const uint32_t qw[3] = {s1.x, s1.y, s1.z};
+  auto q = [&](int j) { return (float)((qw[j >> 2] >> (8 * (j & 3))) & 0xFFu); };  // v_cvt_f32_ubyteN
+  if (tray_fast(r)) {
+    const float ax = sc.x * r.yx, ay = sc.y * r.yy, az = sc.z * r.yz;
+    const float bx = fmaf(o.x, r.yx, -r.oyx), by = fmaf(o.y, r.yy, -r.oyy), bz = fmaf(o.z, r.yz, -r.oyz);
+    const float mabs = fmaf(vmax3(fabsf(bx), fabsf(by), fabsf(bz)), 0x1p-20f, fabsf(r.om));
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int b = 6 * c;
+      const float lx = fmaf(q(b), ax, bx), ly = fmaf(q(b + 1), ay, by), lz = fmaf(q(b + 2), az, bz);
+      const float hx = fmaf(q(b + 3), ax, bx), hy = fmaf(q(b + 4), ay, by), hz = fmaf(q(b + 5), az, bz);
+      const float t0 = vmax3(vmin1(lx, hx), vmin1(ly, hy), vmax1(vmin1(lz, hz), tmin));
+      const float t1 = vmin3(vmax1(lx, hx), vmax1(ly, hy), vmin1(vmax1(lz, hz), tmax));
+      hit[c] = !(t0 - t1 > fmaf(fabsf(t0) + fabsf(t1), 0x1p-19f, mabs));
+      ent[c] = t0;
+    }
+    return;
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int b = 6 * c;
+    auto lo = [&](float qq, float s, float org) {
+      const float p = fmaf(qq, s, org);
+      return p - fmaf(fabsf(p), 0x1p-23f, 0x1p-140f);
+    };
+    auto hi = [&](float qq, float s, float org) {
+      const float p = fmaf(qq, s, org);
+      return p + fmaf(fabsf(p), 0x1p-23f, 0x1p-140f);
+    };
+    const V3 mn{lo(q(b), sc.x, o.x), lo(q(b + 1), sc.y, o.y), lo(q(b + 2), sc.z, o.z)};
+    const V3 mx{hi(q(b + 3), sc.x, o.x), hi(q(b + 4), sc.y, o.y), hi(q(b + 5), sc.z, o.z)};
+    const V3 a = (mn - r.o) / r.d, bb = (mx - r.o) / r.d;  // IEEE quotients (the planes may lie outside the qfast domain)
+    const float t0 = vmax3(vmin1(a.x, bb.x), vmin1(a.y, bb.y), vmax1(vmin1(a.z, bb.z), tmin));
+    const float t1 = vmin3(vmax1(a.x, bb.x), vmax1(a.y, bb.y), vmin1(vmax1(a.z, bb.z), tmax));
+    hit[c] = !(t1 < t0);
+    ent[c] = 0.0f;  // left first
+  }
+}
+
+// The current record is an NF node: both children's boxes tested (culling at
+// best * (1 + 2^-10)); both hit: the nearer next, the other pushed; one: that
+// one; none: the stack's next.
 template <bool COUNT>
 MRT_DEV void trav_box_index_nf(const TravIn& in, const NfStack& k, Trav& t, LocalCounters& lc) {
-  if (COUNT) lc.node_visits++;
-  V3 mn{u2f(t.s0.x), u2f(t.s0.y), u2f(t.s0.z)}, mx{u2f(t.s0.w), u2f(t.s1.x), u2f(t.s1.y)};
-  if (box_hit_any<COUNT>(mn, mx, t.r, in.tmin, nf_cull(t.best), &lc)) {
-    const uint32_t w = t.s1.w, left = w & kNfIdx, axis = (w >> 28) & 3u;
-    if (axis == kNfLeaf) {
-      t.i = left;
-      return;
-    }
-    const float dk = axis == 0 ? t.r.d.x : (axis == 1 ? t.r.d.y : t.r.d.z);
-    const bool l_near = !(dk < 0.0f);
-    nf_push(k, t, l_near ? t.s1.z : left);
-    t.i = l_near ? left : t.s1.z;
+  if (COUNT) lc.node_visits += 2;
+  bool h[2];
+  float e[2];
+  nf_node_test(t.s0, t.s1, t.r, in.tmin, nf_cull(t.best), h, e);
+  const uint32_t base = t.s1.w & kNfIdx, right = base + (t.s0.w >> 24);
+  if (h[0] && h[1]) {
+    const bool lfirst = !(e[1] < e[0]);
+    nf_push(k, t, lfirst ? right : base);
+    t.i = lfirst ? base : right;
+  } else if (h[0] || h[1]) {
+    t.i = h[0] ? base : right;
   } else if (!nf_pop(in, k, t)) {
     nf_over(t);
   }

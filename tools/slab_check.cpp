@@ -73,6 +73,7 @@ float margin(const Ray& r, float t0, float t1) { return std::fma(fabsf(t0) + fab
 
 struct Stats {
   uint64_t boxes = 0, undecided = 0, wrong = 0;
+  uint64_t loads = 0;  // 16-B record loads (k_trace's vector-memory instructions per lane step)
 };
 // path.h box_hit_any's early decision: 1 hit, 0 miss, -1 left to the exact test
 int early_decide(const float mn[3], const float mx[3], const Ray& r, float tmin, float best) {
@@ -139,33 +140,39 @@ Result walk_plain(const HostScene& s, V o, V d, Stats* st = nullptr) {
       const bool truth = box_exact(mn, mx, r, kTmin, best);
       if (st) {
         st->boxes++;
+        st->loads += 2;
         const int dec = early_decide(mn, mx, r, kTmin, best);
         if (dec < 0) st->undecided++;
         else if ((dec != 0) != truth) st->wrong++;
       }
       i = truth ? (k & ~kBoxFlag) : a[6];
     } else if (k == KIND_END) {
+      if (st) st->loads += 2;
       if (ret == ~0u) break;
       if (ret & 0x80000000u) r = wr;
       i = ret & 0x7FFFFFFFu;
       ret = ~0u;
     } else if (k == KIND_SPHERE) {
       float t;
+      if (st) st->loads += 2;
       if (sphere_hit({f(a[0]), f(a[1]), f(a[2])}, f(a[3]), r.o, r.d, kTmin, best, t))
         best = t, prim = MRT_REF(MRT_REF_SPHERE, a[4]), hit_ret = ret;
       i = a[5];  // next (layout.h)
     } else if (k == KIND_TRI) {
       float t;
+      if (st) st->loads += 3;
       if (tri_hit({f(a[0]), f(a[1]), f(a[2])}, {f(a[3]), f(a[4]), f(a[5])}, {f(a[8]), f(a[9]), f(a[10])}, r.o, r.d,
                   kTmin, best, t))
         best = t, prim = MRT_REF(MRT_REF_TRIANGLE, a[6] & kTriIdMask), hit_ret = ret;
       i = a[11];  // next (layout.h)
     } else if (k == KIND_INST) {
       const float* m = &s.inst_inv[12 * (size_t)a[0]];
+      if (st) st->loads += 5;
       r = make_ray(xf(m, wr.o, 1.0f), xf(m, wr.d, 0.0f), s.early_ok);
       ret = (i + 2) | 0x80000000u;
       i = a[1];
     } else if (k == KIND_MODEL) {
+      if (st) st->loads += 2;
       ret = i + 2;
       i = a[1];
     } else {
@@ -179,6 +186,49 @@ Result walk_plain(const HostScene& s, V o, V d, Stats* st = nullptr) {
     cont = MRT_REF((hit_ret & 0x80000000u) ? MRT_REF_INSTANCE : MRT_REF_MODEL, w[4 * (size_t)rec]);
   }
   return {prim, cont, best};
+}
+
+// path.h nf_node_test: both children's boxes of an NF node (layout.h) at
+// once, from the planes' 8-bit steps. Fast rays: t = q * (2^e * y) +
+// (o * y - oy) per plane with the early decision's margin plus the node's
+// |o * y - oy| term — "miss" only when certain, anything else a hit
+// (conservative: the walk's hits are checked, its boxes never need to be
+// exact); other rays: the exact test on the decoded planes widened by an ulp.
+void node_test(const uint32_t* a, const Ray& r, float tmin, float tmax, bool hit[2], float ent[2]) {
+  const float o[3] = {f(a[0]), f(a[1]), f(a[2])};
+  uint8_t q[12];
+  for (int j = 0; j < 3; ++j)
+    for (int b = 0; b < 4; ++b) q[4 * j + b] = (uint8_t)(a[4 + j] >> (8 * b));
+  float sc[3], A[3], B[3], mb = 0.0f;
+  for (int k = 0; k < 3; ++k) {
+    sc[k] = f(((a[3] >> (8 * k)) & 0xFFu) << 23);
+    A[k] = sc[k] * r.y[k];
+    B[k] = std::fma(o[k], r.y[k], -r.oy[k]);
+    mb = std::max(mb, fabsf(B[k]));
+  }
+  const float mabs = std::fma(mb, 0x1p-20f, r.om);
+  for (int c = 0; c < 2; ++c) {
+    const uint8_t* lo = q + 6 * c;
+    const uint8_t* hi = q + 6 * c + 3;
+    if (r.fast) {
+      float tl[3], th[3];
+      for (int k = 0; k < 3; ++k) tl[k] = std::fma((float)lo[k], A[k], B[k]), th[k] = std::fma((float)hi[k], A[k], B[k]);
+      const float t0 = fmaxf(fmaxf(fminf(tl[0], th[0]), fminf(tl[1], th[1])), fmaxf(fminf(tl[2], th[2]), tmin));
+      const float t1 = fminf(fminf(fmaxf(tl[0], th[0]), fmaxf(tl[1], th[1])), fminf(fmaxf(tl[2], th[2]), tmax));
+      const float m = std::fma(fabsf(t0) + fabsf(t1), 0x1p-19f, mabs);
+      hit[c] = !(t0 - t1 > m);
+      ent[c] = t0;
+    } else {
+      float mn[3], mx[3];
+      for (int k = 0; k < 3; ++k) {
+        const float pl = std::fma((float)lo[k], sc[k], o[k]), ph = std::fma((float)hi[k], sc[k], o[k]);
+        mn[k] = pl - std::fma(fabsf(pl), 0x1p-23f, 0x1p-140f);
+        mx[k] = ph + std::fma(fabsf(ph), 0x1p-23f, 0x1p-140f);
+      }
+      hit[c] = box_exact(mn, mx, r, tmin, tmax);
+      ent[c] = 0.0f;
+    }
+  }
 }
 
 // The verified near-first walk (layout.h; path.h trav_*_nf, nf_finish)
@@ -211,7 +261,10 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks) {
         i = v;
         return true;
       }
-      if (ret & 0x80000000u) r = wr;
+      if (ret & 0x80000000u) {
+        r = wr;
+        if (st) st->loads += 2;
+      }
       ret = ~0u;
     }
     return false;
@@ -233,23 +286,22 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks) {
   for (;;) {
     const uint32_t* a = w + 4 * (size_t)i;
     const uint32_t k = a[7];
-    if (k & kBoxFlag) {
-      float mn[3] = {f(a[0]), f(a[1]), f(a[2])}, mx[3] = {f(a[3]), f(a[4]), f(a[5])};
-      if (st) st->boxes++;
-      if (box_exact(mn, mx, r, kTmin, cull())) {
-        const uint32_t left = k & kNfIdx, axis = (k >> 28) & 3u;
-        if (axis == kNfLeaf) {
-          i = left;
-          continue;
-        }
-        const float dk = axis == 0 ? r.d.x : (axis == 1 ? r.d.y : r.d.z);
-        const bool ln = !(dk < 0.0f);
-        stack.push_back(ln ? a[6] : left);
+    if (k & kBoxFlag) {  // a node: both children's boxes, the nearer hit child first
+      if (st) st->boxes += 2, st->loads += 2;
+      bool h[2];
+      float e[2];
+      node_test(a, r, kTmin, cull(), h, e);
+      const uint32_t base = k & kNfIdx, right = base + (a[3] >> 24);
+      if (h[0] && h[1]) {
+        const bool lf = !(e[1] < e[0]);
+        stack.push_back(lf ? right : base);
         if (stack.size() > kNfStack) {
           fprintf(stderr, "nf: stack overflow\n");
           exit(3);
         }
-        i = ln ? left : a[6];
+        i = lf ? base : right;
+      } else if (h[0] || h[1]) {
+        i = h[0] ? base : right;
       } else if (!pop()) {
         break;
       }
@@ -259,6 +311,7 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks) {
     if (k == KIND_TRI) {
       float t;
       const uint32_t pr = MRT_REF(MRT_REF_TRIANGLE, a[6] & kTriIdMask);
+      if (st) st->loads += 3;
       if (tri_hit({f(a[0]), f(a[1]), f(a[2])}, {f(a[3]), f(a[4]), f(a[5])}, {f(a[8]), f(a[9]), f(a[10])}, r.o, r.d,
                   kTmin, cull(), t))
         hit(t, pr);
@@ -266,9 +319,11 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks) {
     } else if (k == KIND_SPHERE) {
       float t;
       const uint32_t pr = MRT_REF(MRT_REF_SPHERE, a[4]);
+      if (st) st->loads += 2;
       if (sphere_hit({f(a[0]), f(a[1]), f(a[2])}, f(a[3]), r.o, r.d, kTmin, cull(), t)) hit(t, pr);
       next = a[5];
     } else if (k == KIND_INST || k == KIND_MODEL) {
+      if (st) st->loads += k == KIND_INST ? 5 : 2;
       if (a[2] != kNfPop) stack.push_back(a[2]);
       stack.push_back(0x80000000u);
       if (k == KIND_INST) {
@@ -297,7 +352,7 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks) {
   auto box_at = [&](uint32_t rec, const Ray& rr) {
     const uint32_t* b = w + 4 * (size_t)rec;
     float mn[3] = {f(b[0]), f(b[1]), f(b[2])}, mx[3] = {f(b[3]), f(b[4]), f(b[5])};
-    if (st) st->boxes++;
+    if (st) st->boxes++, st->loads += 2;
     return box_exact(mn, mx, rr, kTmin, tau);
   };
   if (prim) {
@@ -418,9 +473,10 @@ int main(int argc, char** argv) {
   }
   if (nf) {
     printf("%-14s nf: %llu of %d rays differ from the reference walk; box tests %.1f vs %.1f per ray (x%.2f), "
-           "%llu fallbacks (%.2f%%), stack need %u\n",
+           "record loads %.1f vs %.1f (x%.2f), %llu fallbacks (%.2f%%), stack need %u\n",
            argv[1], (unsigned long long)nf_bad, n, (double)nf_st.boxes / n, (double)st.boxes / n,
-           (double)st.boxes / std::max<uint64_t>(nf_st.boxes, 1), (unsigned long long)nf_fallbacks,
+           (double)st.boxes / std::max<uint64_t>(nf_st.boxes, 1), (double)nf_st.loads / n, (double)st.loads / n,
+           (double)st.loads / std::max<uint64_t>(nf_st.loads, 1), (unsigned long long)nf_fallbacks,
            100.0 * nf_fallbacks / n, s.nf_stack_need);
     if (nf_bad) return 1;
   }
