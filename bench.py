@@ -702,6 +702,36 @@ def config_lines(a, rank, world, dev, devices) -> dict:
     return out
 
 
+def near_first_lines(a, rank, world, dev, devices, exact: dict) -> dict:
+    """The opt-in near-first walk (option traversal=1, massrt.h) on the same
+    workloads as the exact lines: headline, secondary and config 3. Its hits
+    equal the reference walk's except for rays grazing large triangles
+    (DESIGN.md §4 has the measured rates), so it is reported beside the
+    headline, never as `value`."""
+    import copy
+
+    b = copy.copy(a)
+    b.opt = list(a.opt) + ["traversal=1"]
+    out = {"option": "traversal=1 (MRT_TRAVERSAL_NEAR_FIRST)",
+           "exactness": "same hits as the reference walk on every GPU test frame; rays grazing large triangles "
+                        "can differ (DESIGN.md §4: 0-4 in 10^4 of deliberately grazing rays)"}
+    for key, scene, steps, kw in (("headline", a.scene, 2, {}), ("secondary", a.secondary, 2, {}),
+                                  ("c3", "cube_field", 1, dict(spp=1024))):
+        if not scene or scene == "none" or (key == "secondary" and scene == a.scene):
+            continue
+        try:
+            r = run_scene(b, scene, steps, 1, rank, world, dev, False, devices, **kw)
+            ref = exact.get(key)
+            out[key] = {"scene": scene, "workload": r["workload"], "value": r["value"], "ms_per_step": r["ms_per_step"],
+                        "steps": steps, "of_exact": round(r["value"] / ref, 3) if ref else None,
+                        "traversal": r["tuning"].get("traversal"),
+                        "vnf_fallback_frac": (r["roofline"] or {}).get("vnf_fallback_frac"),
+                        "k_trace_avg_launch_ms": ((r["roofline"] or {}).get("k_trace") or {}).get("avg_launch_ms")}
+        except Exception as e:
+            out[key] = {"error": str(e)}
+    return out
+
+
 def main():
     a = parse()
     # --gpus N without a launcher in "ranks" mode: start the N ranks ourselves,
@@ -763,8 +793,12 @@ def main():
                     dropin[sc] = dropin_run(a, sc, ref)
                 except Exception as e:
                     dropin[sc] = {"error": str(e)}
+    near_first = None
     if rank == 0 and solo and not a.no_configs:
         configs = config_lines(a, rank, world, dev, devices)
+        exact = {"headline": head["value"], "secondary": sec["value"] if sec else None,
+                 "c3": (configs.get("c3") or {}).get("value")}
+        near_first = near_first_lines(a, rank, world, dev, devices, exact)
     if cpu:
         try:
             c1 = c1_runs(a)
@@ -814,6 +848,8 @@ def main():
             line["config"]["dropin"] = dropin
         if configs:
             line["config"].update(configs)
+        if near_first:
+            line["config"]["near_first"] = near_first
         if head.get("roofline_k_shade"):
             line["roofline_k_shade"] = head["roofline_k_shade"]
         if head.get("gather"):

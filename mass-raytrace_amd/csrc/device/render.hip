@@ -1012,7 +1012,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"treelet_kb", 0, 0, 150},
     {"trace_block", 256, 256, 1024},
     {"mem_reserve_mb", 4096, 0, 1 << 20},
-    {"traversal", 1, 0, 1},
+    {"traversal", 0, 0, 1},
     {"trace_nf_batch", -1, -1, 64},
 };
 int opt_find(const char* name) {
@@ -1200,8 +1200,9 @@ void set_device(mrt_ctx* c) { HIP_CHECK(hipSetDevice(c->device)); }
 //  * k_shade at 7 waves/SIMD for a big non-instanced world (mesh_ply 948.6
 //    -> 969.0), else 8 (sphere_grid 808.8, 7: 778.1; profiles/r3_tune2/wpe.txt).
 //  The near-first walk (round 4, profiles/r4_nf/tune.txt) has rules of its
-//  own: refill 24 and box run >= 28 lanes for a big non-instanced world
-//  (mesh_ply 1383.7 -> 1432.6), 512 rays per grab except there (cube_field
+//  own: refill 40 except for a big non-instanced world (sphere_grid 1106.9
+//  -> 1137.4, cube_field 608.6 -> 614.6; mesh_ply 1581.6 -> 1528.7 keeps 32)
+//  and box run >= 28 lanes there, 512 rays per grab except there (cube_field
 //  556.2 -> 580.2 with shade 7; mesh_ply keeps 128: 1386.7 vs 1372.7), and
 //  k_shade at 7 waves/SIMD everywhere (sphere_grid 983.3 -> 992.9).
 void apply_options(mrt_ctx* c) {
@@ -1216,7 +1217,7 @@ void apply_options(mrt_ctx* c) {
   c->finish_paths = (uint32_t)o[OPT_FINISH_PATHS];
   c->finish_grid_div = (uint32_t)o[OPT_FINISH_GRID_DIV];
   c->tune.refill = o[OPT_TRACE_REFILL] >= 0 ? (uint32_t)std::max<int64_t>(1, o[OPT_TRACE_REFILL])
-                                            : ((nf && big_solid) ? 24u : 32u);
+                                            : ((nf && !big_solid) ? 40u : 32u);
   c->tune.box_min = o[OPT_TRACE_BOX_MIN] >= 0 ? (uint32_t)std::max<int64_t>(1, o[OPT_TRACE_BOX_MIN])
                                               : (inst ? 16u : (big ? (nf ? 28u : 32u) : 24u));
   c->tune.chunk = o[OPT_TRACE_CHUNK] >= 0 ? (uint32_t)o[OPT_TRACE_CHUNK]
@@ -1299,14 +1300,15 @@ void wait_queues(mrt_ctx* c, hipStream_t st) {
 // and shade launches find room on every CU instead of queueing behind a
 // grid that holds the whole GPU until its last ray (sphere_grid, 2 queues:
 // 8 WGs/CU 585, 6 WGs/CU 618 Msamples/s).
-uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem, bool shared = false, int block = kBlock) {
+uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem, bool shared = false, int block = kBlock,
+                         int share_num = 3, int share_den = 4) {
   auto key = std::make_pair(f, smem);
   auto it = c->grids.find(key);
   if (it != c->grids.end()) return it->second;
   if (smem > 0) HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTraceLdsMaxBytes));
   int per_cu = 0;
   HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, smem));
-  if (shared) per_cu = std::max(1, per_cu * 3 / 4);
+  if (shared) per_cu = std::max(1, per_cu * share_num / share_den);
   if (c->wgs_per_cu) per_cu = (int)c->wgs_per_cu;
   const uint32_t g = (uint32_t)c->cus * (uint32_t)std::max(1, per_cu);
   c->grids[key] = g;
@@ -1358,9 +1360,11 @@ void launch_trace_nf(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs&
   const void* f = count ? (const void*)k_trace<true, false, ALPHA, false, kBlock, true>
                         : (const void*)k_trace<false, false, ALPHA, false, kBlock, true>;
   // 80 VGPRs and kNfStack KiB of LDS per workgroup both allow 6 waves per
-  // SIMD: a full grid leaves the other queue's k_shade no VGPRs, so the walk
-  // takes the 3/4 share like the reference walk's grid
-  const uint32_t grid = persistent_grid(c, f, smem, c->n_queues > 1, kBlock);
+  // SIMD: a full grid leaves the other queue's k_shade no VGPRs. The walk
+  // takes half (3 of 6 WG/CU): its vector-memory unit is the shared limit, so
+  // more of its waves buy nothing while k_shade beside it gains (profiles/
+  // r4_nf/tune.txt §6: 4 -> 3 WG/CU +0.8%, 2 WG/CU -14%)
+  const uint32_t grid = persistent_grid(c, f, smem, c->n_queues > 1, kBlock, 1, 2);
   if (count)
     hipLaunchKernelGGL((k_trace<true, false, ALPHA, false, kBlock, true>), dim3(grid), dim3(kBlock), smem, st, c->S, in,
                        q.hits, q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
