@@ -378,7 +378,34 @@ struct TravIn {
   float tmin;
   uint4* rng = nullptr;    // the rays' RNG states (traversal draws: Volume, Mix alpha tests)
   float tmax0 = INFINITY;  // the walk's initial t_max (a near-first lane that falls back restarts with it)
+  // k_trace (reference walk, no treelet): this lane's 4 x 16 B of LDS, stride
+  // `stash_stride` float4s, holding the world ray while the lane is inside an
+  // instance's BLAS — leaving it then costs 4 LDS reads instead of 2 pool
+  // loads and make_tray's four correctly rounded divisions (nullptr: recompute)
+  float4* stash = nullptr;
+  uint32_t stash_stride = 0;
 };
+MRT_DEV void tray_stash(const TravIn& in, const TRay& r) {
+  float4* p = in.stash;
+  const uint32_t k = in.stash_stride;
+  p[0] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+  p[k] = make_float4(r.d.y, r.d.z, r.yx, r.yy);
+  p[2 * k] = make_float4(r.yz, r.oyx, r.oyy, r.oyz);
+  p[3 * k] = make_float4(r.om, r.a.b, r.a.y, 0.0f);
+}
+MRT_DEV TRay tray_unstash(const TravIn& in) {
+  const float4* p = in.stash;
+  const uint32_t k = in.stash_stride;
+  const float4 a = p[0], b = p[k], c = p[2 * k], e = p[3 * k];
+  TRay r;
+  r.o = V3{a.x, a.y, a.z};
+  r.d = V3{a.w, b.x, b.y};
+  r.yx = b.z, r.yy = b.w, r.yz = c.x;
+  r.oyx = c.y, r.oyy = c.z, r.oyz = c.w;
+  r.om = e.x;
+  r.a.b = e.y, r.a.y = e.z;
+  return r;
+}
 
 // Inside a BLAS, `ret` is the world record after the instance/model record
 // that entered it, with kRetInstance set for an instance; the container of a
@@ -543,7 +570,7 @@ MRT_DEV void trav_end_index(const TravIn& in, Trav& t) {
     t.done = true;
     return;
   }
-  if (t.ret & kRetInstance) t.r = world_ray(in, t.ray);
+  if (t.ret & kRetInstance) t.r = in.stash ? tray_unstash(in) : world_ray(in, t.ray);
   t.i = t.ret & ~kRetInstance;
   t.ret = kNoRet;
 }
@@ -672,6 +699,7 @@ MRT_DEV void trav_prim_index(const TravIn& in, Trav& t, LocalCounters& lc) {
     V3 c0, c1, c2, c3;
     load_m12(S.inst_inv + (size_t)MRT_IDX(S, s0.x, S.n_inst, 8) * 12, c0, c1, c2, c3);
     // entered from the world region: t.r is the world ray here
+    if (in.stash) tray_stash(in, t.r);
     t.r = make_tray(xform(c0, c1, c2, c3, t.r.o, 1.0f), xform(c0, c1, c2, c3, t.r.d, 0.0f), S.fast_ok);
     t.ret = (t.i + 2) | kRetInstance;
     t.i = s0.y;

@@ -257,6 +257,7 @@ struct TraceTune {
 // workgroup share one copy.
 constexpr size_t kTraceLdsMaxBytes = 160 * 1024;
 constexpr uint32_t kIdle = 0xFFFFFFFFu;  // Trav.ray of a lane without a ray
+constexpr uint32_t kStashQuads = 4;      // float4s per lane of the world-ray stash (TravIn::stash)
 
 // RNG: the scene's traversal draws random numbers (Volume, Mix alpha tests):
 // each ray carries its path stream through the traversal and stores it back.
@@ -278,8 +279,13 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(NF ? (COUNT
     for (uint32_t k = threadIdx.x; k < S.n_tlet; k += BLK) mrt_lds[k] = reinterpret_cast<const uint4*>(S.tlet)[k];
     __syncthreads();
   }
-  const TravIn tin{S, reinterpret_cast<const uint4*>(LDS ? S.slots_tl : S.slots), LDS ? S.tl_world_begin : S.world_begin,
-                   in.ro, in.rd, tmin, in.rng, tmax};
+  TravIn tin_{S, reinterpret_cast<const uint4*>(LDS ? S.slots_tl : S.slots), LDS ? S.tl_world_begin : S.world_begin,
+              in.ro, in.rd, tmin, in.rng, tmax};
+  if (!LDS && !NF) {  // the reference walk without a treelet: LDS holds the world-ray stash (TravIn::stash)
+    tin_.stash = reinterpret_cast<float4*>(mrt_lds) + threadIdx.x;
+    tin_.stash_stride = (uint32_t)BLK;
+  }
+  const TravIn& tin = tin_;
   const NfStack stk{reinterpret_cast<uint32_t*>(mrt_lds) + threadIdx.x, (uint32_t)BLK};
   LocalCounters lc;
   uint32_t seg = 0, nh = 0;
@@ -1318,7 +1324,8 @@ uint32_t persistent_grid(mrt_ctx* c, const void* f, size_t smem, bool shared = f
 template <bool LDS, uint32_t ALPHA, bool RNG, int BLK>
 void launch_trace_b(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in, uint32_t cur, bool count,
                     float tmin, float tmax) {
-  const size_t smem = LDS ? (size_t)c->S.n_tlet * 16 : 0;
+  // no treelet: 4 x 16 B per lane for the world-ray stash (TravIn::stash)
+  const size_t smem = LDS ? (size_t)c->S.n_tlet * 16 : (size_t)kStashQuads * BLK * 16;
   const void* f = count ? (const void*)k_trace<true, LDS, ALPHA, RNG, BLK> : (const void*)k_trace<false, LDS, ALPHA, RNG, BLK>;
   const uint32_t grid = persistent_grid(c, f, smem, c->n_queues > 1, BLK);
   if (count)

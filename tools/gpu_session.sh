@@ -53,7 +53,7 @@ case $MODE in
     for lib in "$@"; do
       lab=${labels[$k]:-$(basename $lib .so)}; k=$((k + 1))
       for sc in $SCENES; do
-        MASSRT_LIB=$lib quick "$lab" gpurun_out/session/ab_${lab}_$sc.log --scene $sc --steps $STEPS || exit 1
+        MASSRT_LIB=$lib quick "$lab" gpurun_out/session/ab_${lab}_$sc.log --scene $sc --steps $STEPS $BENCH_ARGS || exit 1
       done
     done ;;
   sweep)

@@ -415,13 +415,18 @@ int main(int argc, char** argv) {
   const bool layout = argc > 4 && !strcmp(argv[4], "layout");
   // `nf` mode: the verified near-first walk must find the reference's closest
   // hits (primitive, container, t bits) on every ray
-  const bool nf = argc > 4 && (!strcmp(argv[4], "nf") || !strcmp(argv[4], "graze"));
+  const bool nf = argc > 4 && (!strcmp(argv[4], "nf") || !strcmp(argv[4], "graze") || !strcmp(argv[4], "tangent"));
   // `graze` mode: rays nearly parallel to a triangle of the scene (angle
   // 10^U(-8,-1.5) rad to its plane, through a random point of it, from 0.5-60
   // units back; through an instance's transform half the time) — where
   // Moller-Trumbore's t is least accurate, the near-first walk's culling
   // margin is tested hardest
   const bool graze = argc > 4 && !strcmp(argv[4], "graze");
+  // `tangent` mode: rays nearly tangent to a sphere (offset 10^U(-7,-1) of its
+  // radius from the tangent line) from 1-400 radii away — where the sphere
+  // test's disc cancels
+  const bool tangent = argc > 4 && !strcmp(argv[4], "tangent");
+  const bool stress = graze || tangent;
   if (nf && !s.nf_ok) {
     printf("%-14s nf: no near-first trees (%s)\n", argv[1], s.nf_note.c_str());
     return 0;
@@ -440,7 +445,23 @@ int main(int argc, char** argv) {
   V cam_d{0, 0, -1};
   for (int k = 0; k < n; ++k) {
     V ro, rd;
-    if (graze) {
+    if (tangent) {
+      if (!d.n_spheres) break;
+      const mrt_sphere& sp = d.spheres[std::min<uint32_t>(d.n_spheres - 1, (uint32_t)(u(g) * d.n_spheres))];
+      const float rad = fabsf(sp.radius);
+      V w{u(g) * 2 - 1, u(g) * 2 - 1, u(g) * 2 - 1};
+      const float wl = sqrtf(dot(w, w));
+      if (!(wl > 0.1f)) continue;
+      w = {w.x / wl, w.y / wl, w.z / wl};  // from the centre towards the tangent point
+      V t1 = cross(w, fabsf(w.x) < 0.9f ? V{1, 0, 0} : V{0, 1, 0});
+      const float tl = sqrtf(dot(t1, t1));
+      t1 = {t1.x / tl, t1.y / tl, t1.z / tl};
+      const float off = rad * (1.0f + (u(g) < 0.5f ? -1.0f : 1.0f) * powf(10.0f, -7.0f + 6.0f * u(g)));
+      const V p{sp.center[0] + w.x * off, sp.center[1] + w.y * off, sp.center[2] + w.z * off};
+      const float sc = 0.5f + 1.5f * u(g), back = rad * powf(10.0f, 2.6f * u(g));
+      rd = {t1.x * sc, t1.y * sc, t1.z * sc};
+      ro = {p.x - rd.x * back / sc, p.y - rd.y * back / sc, p.z - rd.z * back / sc};
+    } else if (graze) {
       const mrt_triangle& tr = d.triangles[std::min<uint32_t>(d.n_triangles - 1, (uint32_t)(u(g) * d.n_triangles))];
       const float* m = nullptr;
       if (d.n_instances && u(g) < 0.5f)
@@ -514,7 +535,7 @@ int main(int argc, char** argv) {
            (double)st.boxes / std::max<uint64_t>(nf_st.boxes, 1), (double)nf_st.loads / n, (double)st.loads / n,
            (double)st.loads / std::max<uint64_t>(nf_st.loads, 1), (unsigned long long)nf_fallbacks,
            100.0 * nf_fallbacks / n, s.nf_stack_need);
-    if (nf_bad && !graze) return 1;
+    if (nf_bad && !stress) return 1;
   }
   if (layout) {
     printf("%-14s layout: %llu of %d rays differ between the sibling layout and the preorder stream; stream %zu vs %zu slots\n",
