@@ -377,24 +377,24 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(NF ? (COUNT
       const bool at_box = busy && trav_at_box(t[q]);
       const unsigned long long box_mask = __ballot(at_box);
       const unsigned long long prim_mask = __ballot(busy && !at_box);
-      if (at_box) {
-        if (NF && t[q].sp != kExactMode) {
-          trav_box_index_nf<COUNT>(tin, stk, t[q], lc);
-          if (t[q].sp != kNfDone) trav_fetch<LDS>(tin, t[q]);
-        } else {
-          trav_box<COUNT, LDS>(tin, t[q], lc);
-        }
-      }
-      // primitives wait until enough lanes are at one (or no lane is at a box)
+      // one step per busy lane (a box, or a primitive once enough lanes wait
+      // at one or no lane is at a box), then ONE record fetch for every lane
+      // that moved: the address unit costs per wave instruction, so the box
+      // and primitive lanes share the load pair instead of issuing one each
       const bool prim_go = (__popcll(prim_mask) >= tune.prim_batch || box_mask == 0) && busy && !at_box;
-      if (prim_go) {
-        if (NF && t[q].sp != kExactMode) {
-          trav_prim_index_nf<COUNT, ALPHA>(tin, stk, t[q], lc);
-          if (t[q].sp != kNfDone) trav_fetch<LDS>(tin, t[q]);
-        } else {
-          trav_prim<COUNT, ALPHA, RNG, LDS>(tin, t[q], lc);
-        }
+      if (at_box) {
+        if (NF && t[q].sp != kExactMode)
+          trav_box_index_nf<COUNT>(tin, stk, t[q], lc);
+        else
+          trav_box_index<COUNT>(tin, t[q], lc);
       }
+      if (prim_go) {
+        if (NF && t[q].sp != kExactMode)
+          trav_prim_index_nf<COUNT, ALPHA>(tin, stk, t[q], lc);
+        else
+          trav_prim_index<COUNT, ALPHA, RNG, LDS>(tin, t[q], lc);
+      }
+      if ((at_box || prim_go) && !t[q].done && (!NF || t[q].sp != kNfDone)) trav_fetch<LDS>(tin, t[q]);
       // near-first walks that are over: check their hits (done, or the
       // reference's walk from the start) — batched: the check is a few
       // hundred wave instructions, so finished lanes wait (holding an END
