@@ -356,7 +356,7 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  * computed t undercuts its own box by more than the culling margin, which
  * Moller-Trumbore's t can do for rays nearly parallel to a large triangle:
  * no difference in the GPU test frames; 1 to 4 in 10^4 of deliberately
- * grazing rays (DESIGN.md §4 lists the rates). 1.3-4x faster. Counters
+ * grazing rays (DESIGN.md §4 lists the rates). 1.3-1.5x faster (Menger ~3x). Counters
  * (node visits, ...) then count its work. */
 #define MRT_TRAVERSAL_REFERENCE 0
 #define MRT_TRAVERSAL_NEAR_FIRST 1
