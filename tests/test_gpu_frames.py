@@ -171,13 +171,19 @@ def test_options_and_tuning(scene, golden_dir):
     c.upload(scene)
     t = c.tuning()
     assert t["queues"] == 2 and t["trace_box_min"] == 24 and t["trace_chunk"] == 512 and t["shade_waves"] == 8
+    assert c.get_option("traversal") == massrt.TRAVERSAL_REFERENCE and t["traversal"] == massrt.TRAVERSAL_REFERENCE
+    c.set_option("traversal", massrt.TRAVERSAL_NEAR_FIRST)  # its own rules: refill 40, k_shade at 7
+    t = c.tuning()
+    assert t["traversal"] == massrt.TRAVERSAL_NEAR_FIRST and t["trace_refill"] == 40 and t["shade_waves"] == 7
+    c.set_option("traversal", massrt.TRAVERSAL_REFERENCE)
     c.set_option("trace_box_min", 40)
     assert c.tuning()["trace_box_min"] == 40 and c.get_option("trace_box_min") == 40
     cube = massrt.Builder(1).builtin("cube_field", ASPECT, golden_dir)
     c.set_option("trace_box_min", -1)
     c.upload(cube)  # > 1000 instances: box run from 16 lanes, grabs of 128
     assert c.tuning()["trace_box_min"] == 16 and c.tuning()["trace_chunk"] == 128
-    for name, bad in (("queues", 5), ("trace_block", 300), ("shade_waves", 6), ("trace_chunk", 8)):
+    for name, bad in (("queues", 5), ("trace_block", 300), ("shade_waves", 6), ("trace_chunk", 8), ("trace_nf_batch", 0),
+                      ("traversal", 2)):
         with pytest.raises(massrt.MassrtError, match=name):
             c.set_option(name, bad)
     with pytest.raises(massrt.MassrtError, match="unknown option"):
