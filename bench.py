@@ -333,7 +333,7 @@ def load_pmc(path: Path, stamp: dict):
         pj = json.loads(path.read_text())
     except (OSError, ValueError):
         return None
-    st = {"n_gpus": 1, **pj.get("stamp", {})}  # profiles are taken on one GPU
+    st = {"n_gpus": 1, "traversal": 0, **pj.get("stamp", {})}  # profiles are taken on one GPU, the reference walk unless stamped
     if any(st.get(k) != v for k, v in stamp.items()):
         return None
     return pj
@@ -523,9 +523,15 @@ def roofline_for(a, scene, cnt, ks, samples_total, elapsed, n_gpus, plan) -> tup
     bytes_per_launch = bytes_per_seg * segs / trav_launches
     avg_ms = (ks["trace_ms"] + fin_ms) / trav_launches
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    import massrt
+
+    # the walk the run used (option traversal): its own profile, profiles/pmc_<scene>_nf.json for the near-first walk
+    trav = int({**massrt.env_options(), **context_options(a)}.get("traversal", 0))
     stamp = {"scene": scene, "width": a.width, "height": a.height, "spp_per_step": plan["spp_per_step"],
-             "src": src_hash(), "n_gpus": n_gpus}
-    pmc_path = Path(a.pmc_json) if (a.pmc_json and scene == a.scene) else REPO / "profiles" / f"pmc_{scene}.json"
+             "src": src_hash(), "n_gpus": n_gpus, "traversal": trav}
+    tag = "_nf" if trav else ""
+    pmc_path = (Path(a.pmc_json) if (a.pmc_json and scene == a.scene and not trav)
+                else REPO / "profiles" / f"pmc_{scene}{tag}.json")
     pj = load_pmc(pmc_path, stamp)
     lim = limiter(pj) if pj else {}
     traffic = pj["kernels"]["k_trace"].get("hbm_bytes_per_launch") if pj else None

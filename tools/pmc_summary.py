@@ -19,6 +19,7 @@ and configuration it measured; bench.py ignores a file whose stamp differs.
 import csv
 import glob
 import json
+import os
 import sys
 from collections import defaultdict
 from pathlib import Path
@@ -59,7 +60,10 @@ def short(name):
 import bench  # noqa: E402  (source hash of the library the profile measured)
 
 summary = {"scene": scene, "width": W, "height": H,
-           "stamp": {"scene": scene, "width": W, "height": H, "spp_per_step": SPP, "src": bench.src_hash()},
+           "stamp": {"scene": scene, "width": W, "height": H, "spp_per_step": SPP, "src": bench.src_hash(),
+                     # the walk profiled (MASSRT_OPTIONS traversal=1: the near-first walk, TAG=_nf)
+                     "traversal": int(dict(kv.split("=") for kv in os.environ.get("MASSRT_OPTIONS", "").split(",")
+                                           if "=" in kv).get("traversal", 0))},
            "kernels": {}}
 for r in rows("trace/**/*kernel_stats.csv"):
     name = short(r.get("Name", r.get("KernelName", "")))
@@ -112,7 +116,7 @@ t = summary["kernels"].get("k_trace", {})
 if "hbm_bytes_per_launch" in t:
     summary["k_trace_hbm_bytes_per_launch"] = t["hbm_bytes_per_launch"]
 print(json.dumps(summary, indent=1))
-import os  # noqa: E402
+
 
 tag = os.environ.get("PMC_TAG", "")
 if tag:
