@@ -86,6 +86,11 @@ void pad_box(Box& b, float rel_extra) {
   for (int k = 0; k < 3; ++k) b.mn[k] = pad(b.mn[k], -1.0f, rel_extra), b.mx[k] = pad(b.mx[k], 1.0f, rel_extra);
 }
 
+// NF triangle boxes are thickened by this fraction of the triangle's extent
+// (object_box): grazing rays, whose computed t can undercut the plane far
+// more than the culling margin, then meet the box before the plane
+constexpr float kTriThick = 0x1p-6f;
+
 // ---- binned SAH over items ----
 struct Item {
   Box b;
@@ -364,6 +369,17 @@ struct Builder {
         b.grow(t.b[0], t.b[1], t.b[2]);
         b.grow(t.c[0], t.c[1], t.c[2]);
         pad_box(b, 0.0f);
+        // a slab of kTriThick x the triangle's extent on every side: a ray
+        // grazing the triangle at angle a enters the box h / sin(a) before
+        // the plane, while Moller-Trumbore's t can undercut the plane by
+        // ~dist * eps / sin(a) — the sin(a) cancels, so hits within
+        // ext * kTriThick / (c * eps) of the ray origin (~10^5 x the
+        // triangle's extent) can never be culled
+        {
+          float ext = 0.0f;
+          for (int k = 0; k < 3; ++k) ext = fmaxf(ext, b.mx[k] - b.mn[k]);
+          for (int k = 0; k < 3; ++k) b.mn[k] -= ext * kTriThick, b.mx[k] += ext * kTriThick;
+        }
         break;
       }
       case KIND_INST:
