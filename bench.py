@@ -719,8 +719,8 @@ def near_first_lines(a, rank, world, dev, devices, exact: dict) -> dict:
     b = copy.copy(a)
     b.opt = list(a.opt) + ["traversal=1"]
     out = {"option": "traversal=1 (MRT_TRAVERSAL_NEAR_FIRST)",
-           "exactness": "same hits as the reference walk on every GPU test frame; rays grazing large triangles "
-                        "can differ (DESIGN.md §4: 0-4 in 10^4 of deliberately grazing rays)"}
+           "exactness": "same hits as the reference walk on every GPU test frame and on 1.2M adversarial "
+                        "grazing/tangent rays (DESIGN.md §4); not proven exact, so never the headline"}
     for key, scene, steps, kw in (("headline", a.scene, 2, {}), ("secondary", a.secondary, 2, {}),
                                   ("c3", "cube_field", 1, dict(spp=1024))):
         if not scene or scene == "none" or (key == "secondary" and scene == a.scene):

@@ -354,9 +354,10 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  * ancestors pass BoundingBox::hit at that t) and walks the reference's way
  * where it does not. Its hits equal the reference's unless a primitive's
  * computed t undercuts its own box by more than the culling margin, which
- * Moller-Trumbore's t can do for rays nearly parallel to a large triangle:
- * no difference in the GPU test frames; 1 to 4 in 10^4 of deliberately
- * grazing rays (DESIGN.md §4 lists the rates). 1.3-1.5x faster (Menger ~3x). Counters
+ * Moller-Trumbore's t can do for rays nearly parallel to a large triangle;
+ * the walk's triangle boxes are thickened against it, and no difference
+ * was found in the GPU test frames nor in 1.2M adversarial grazing/tangent
+ * rays, but it is not proven. 1.25-1.46x faster (Menger ~3x). Counters
  * (node visits, ...) then count its work. */
 #define MRT_TRAVERSAL_REFERENCE 0
 #define MRT_TRAVERSAL_NEAR_FIRST 1
