@@ -432,6 +432,7 @@ int main(int argc, char** argv) {
     return 0;
   }
   uint64_t nf_bad = 0, nf_fallbacks = 0;
+  std::vector<uint32_t> nf_per_ray, ref_per_ray;  // box tests per ray: the tail a persistent wave waits on
   Stats nf_st;
   if (layout) {
     if (!build_host_scene(d, dfs, err, false)) return 1;
@@ -509,7 +510,10 @@ int main(int argc, char** argv) {
     const Result r = walk_plain(s, ro, rd, &st);
     hits += r.prim != 0;
     if (nf) {
+      const uint64_t nb0 = nf_st.boxes;
       const Result q = walk_nf(s, ro, rd, &nf_st, &nf_fallbacks);
+      nf_per_ray.push_back(uint32_t(nf_st.boxes - nb0));
+      ref_per_ray.push_back(uint32_t(st.boxes - boxes0));
       uint32_t tb, qb;
       memcpy(&tb, &r.t, 4);
       memcpy(&qb, &q.t, 4);
@@ -535,6 +539,14 @@ int main(int argc, char** argv) {
            (double)st.boxes / std::max<uint64_t>(nf_st.boxes, 1), (double)nf_st.loads / n, (double)st.loads / n,
            (double)st.loads / std::max<uint64_t>(nf_st.loads, 1), (unsigned long long)nf_fallbacks,
            100.0 * nf_fallbacks / n, s.nf_stack_need);
+    auto tail = [](std::vector<uint32_t> v, double q) {
+      if (v.empty()) return 0u;
+      std::sort(v.begin(), v.end());
+      return v[std::min<size_t>(v.size() - 1, size_t(q * v.size()))];
+    };
+    printf("%-14s nf tail: box tests per ray p99 %u / p99.9 %u / max %u (reference walk %u / %u / %u)\n", argv[1],
+           tail(nf_per_ray, 0.99), tail(nf_per_ray, 0.999), tail(nf_per_ray, 1.0), tail(ref_per_ray, 0.99),
+           tail(ref_per_ray, 0.999), tail(ref_per_ray, 1.0));
     if (nf_bad && !stress) return 1;
   }
   if (layout) {
