@@ -353,11 +353,12 @@ def limiter(pj: dict, kernel: str = "k_trace"):
 
 
 def context_options(a) -> dict:
-    """--opt NAME=VALUE (mrt_set_option); MASSRT_OPTIONS adds to them (massrt.env_options)."""
-    out = {}
-    for item in a.opt:
-        k, _, v = item.partition("=")
-        out[k.strip()] = int(v)
+    """MASSRT_OPTIONS (massrt.env_options), then --opt NAME=VALUE on top: the
+    options bench.py's contexts are created with (mrt_set_option)."""
+    import massrt
+
+    out = massrt.env_options()
+    out.update(massrt.parse_options(",".join(a.opt), "--opt"))
     return out
 
 
@@ -526,7 +527,7 @@ def roofline_for(a, scene, cnt, ks, samples_total, elapsed, n_gpus, plan) -> tup
     import massrt
 
     # the walk the run used (option traversal): its own profile, profiles/pmc_<scene>_nf.json for the near-first walk
-    trav = int({**massrt.env_options(), **context_options(a)}.get("traversal", 0))
+    trav = int(context_options(a).get("traversal", 0))
     stamp = {"scene": scene, "width": a.width, "height": a.height, "spp_per_step": plan["spp_per_step"],
              "src": src_hash(), "n_gpus": n_gpus, "traversal": trav}
     tag = "_nf" if trav else ""

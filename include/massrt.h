@@ -357,7 +357,9 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  * Moller-Trumbore's t can do for rays nearly parallel to a large triangle;
  * the walk's triangle boxes are thickened against it, and no difference
  * was found in the GPU test frames nor in 1.2M adversarial grazing/tangent
- * rays, but it is not proven. 1.25-1.46x faster (Menger ~3x). Counters
+ * rays, but it is not proven. Measured round 4: 1.25x / 1.41x /
+ * 1.46x the reference walk on sphere_grid / mesh_ply / cube_field, but 0.56x on
+ * Menger (a 4.19M-node TLAS: trace_nf_batch 64 brings it to ~1.0x). Counters
  * (node visits, ...) then count its work. */
 #define MRT_TRAVERSAL_REFERENCE 0
 #define MRT_TRAVERSAL_NEAR_FIRST 1
@@ -407,7 +409,9 @@ int mrt_shard_unpack_device(mrt_ctx* ctx, uint32_t width, uint32_t height, uint3
  * at once; if that fails the context falls back to peer copies and
  * mrt_context_transport says why. Every pixel is summed on one device only,
  * so the image equals the one-device render bit for bit. mrt_render with
- * host buffers sends each device only its own shard's pixels.
+ * host buffers uploads the caller's whole buffers to devices[0] and only
+ * their own shard's pixels to the others, and copies the whole frame back:
+ * pixels outside this call's shards come back as the caller had them.
  * On such a context mrt_upload_scene, mrt_set_camera and mrt_render (host
  * buffers) use every device; mrt_get/reset_counters and mrt_get/reset_
  * kernel_stats sum over them; every other entry point runs on devices[0]

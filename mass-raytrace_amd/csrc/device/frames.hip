@@ -313,10 +313,12 @@ int multi_render(MultiDev* m, const mrt_render_args* a, float* rgb, uint32_t* bo
     if (f.d.empty() || f.W != a->width || f.H != a->height || f.si != a->shard_index || f.sc != sc)
       f.setup(m, m->devs, a->width, a->height, a->shard_index, sc);
     const size_t n = f.npix();
-    // every device starts from the caller's sums of ITS shard's pixels (what
-    // it adds to): each gets only those, packed on the host into its slab
-    // and unpacked on the device; the others' pixels arrive with the gather,
-    // so device 0's buffer comes back whole
+    // Device 0 starts from the caller's whole buffers: after the gather it
+    // holds every device's shards, and every other pixel of the frame (the
+    // other processes' shards when shard_count > 1) stays as the caller had
+    // it, so the copy back below returns the caller's sums there unchanged.
+    // Devices 1.. start from the caller's sums of their own shard's pixels
+    // only (what they add to), packed on the host into their slab.
     {
       std::vector<Fail> fails(f.d.size(), Fail{MRT_OK, ""});
       std::vector<std::thread> th;
@@ -324,6 +326,13 @@ int multi_render(MultiDev* m, const mrt_render_args* a, float* rgb, uint32_t* bo
         th.emplace_back([&, i] {
           try {
             DevFrame& d = f.d[i];
+            HIPF(hipSetDevice(d.device));
+            if (i == 0) {
+              HIPF(hipMemcpyAsync(d.rgb, rgb, n * 12, hipMemcpyHostToDevice, d.st));
+              HIPF(hipMemcpyAsync(d.b, bounces, n * 4, hipMemcpyHostToDevice, d.st));
+              HIPF(hipStreamSynchronize(d.st));
+              return;
+            }
             if (!d.count) return;
             std::vector<uint32_t> slab((size_t)d.count * 4);
             for (uint32_t k = 0; k < d.count; ++k) {
@@ -331,7 +340,6 @@ int multi_render(MultiDev* m, const mrt_render_args* a, float* rgb, uint32_t* bo
               memcpy(&slab[4 * (size_t)k], rgb + 3 * (size_t)p, 12);
               slab[4 * (size_t)k + 3] = bounces[p];
             }
-            HIPF(hipSetDevice(d.device));
             HIPF(hipMemcpyAsync(d.slab, slab.data(), slab.size() * 4, hipMemcpyHostToDevice, d.st));
             MRTF(d.ctx, mrt_shard_unpack_device(d.ctx, f.W, f.H, f.shard(i), f.shards(), d.slab, d.rgb, d.b, d.st));
             HIPF(hipStreamSynchronize(d.st));  // the host slab goes out of scope

@@ -17,6 +17,7 @@
 #include <string.h>
 
 #include <array>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <string>
@@ -1068,7 +1069,7 @@ struct Queue {
 struct mrt_ctx {
   int device = 0;
   MultiDev* multi = nullptr;  // a context over several devices (frames.hip): the rest is unused
-  int images = 0;             // live mrt_image objects created on this handle
+  std::atomic<int> images{0};  // live mrt_image objects created on this handle (any thread)
   hipStream_t stream = nullptr;
   std::string err;
   // scene
@@ -1988,7 +1989,7 @@ extern "C" {
 int mrt_destroy(mrt_ctx* c) {
   if (!c) return MRT_OK;
   if (c->images > 0) {  // an image holds the per-device contexts (massrt.h)
-    c->err = "mrt_destroy: " + std::to_string(c->images) + " image(s) of this context still exist";
+    c->err = "mrt_destroy: " + std::to_string(c->images.load()) + " image(s) of this context still exist";
     g_last_error = c->err;
     return MRT_ERR_STATE;
   }

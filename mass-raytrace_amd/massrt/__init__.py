@@ -161,17 +161,27 @@ GATHER_AUTO, GATHER_PEER, GATHER_RCCL = 0, 1, 2
 TRAVERSAL_REFERENCE, TRAVERSAL_NEAR_FIRST = 0, 1
 
 
-def env_options(env=None) -> dict:
-    """Options for every Context this process creates, from MASSRT_OPTIONS
-    ("queues=1,treelet_kb=16"): the harness's way for tools/ scripts to A/B a
-    knob through bench.py. The library itself never reads the environment;
-    options reach it only through mrt_set_option."""
-    text = (os.environ if env is None else env).get("MASSRT_OPTIONS", "")
+def parse_options(text: str, what: str = "options") -> dict:
+    """"queues=1,treelet_kb=16" -> {"queues": 1, "treelet_kb": 16}; a malformed
+    item raises ValueError naming it."""
     out = {}
     for item in filter(None, (x.strip() for x in text.split(","))):
-        k, _, v = item.partition("=")
-        out[k.strip()] = int(v)
+        k, eq, v = item.partition("=")
+        try:
+            if not eq or not k.strip():
+                raise ValueError
+            out[k.strip()] = int(v, 0)
+        except ValueError:
+            raise ValueError(f"{what}: item {item!r} is not NAME=INTEGER") from None
     return out
+
+
+def env_options(env=None) -> dict:
+    """MASSRT_OPTIONS ("queues=1,treelet_kb=16") parsed: the harness's way for
+    tools/ scripts to A/B a knob through bench.py, which passes the result as
+    Context(options=...). Neither the library nor Context reads the
+    environment; options reach a context only through mrt_set_option."""
+    return parse_options((os.environ if env is None else env).get("MASSRT_OPTIONS", ""), "MASSRT_OPTIONS")
 
 
 # scheduling counters of the persistent k_trace (no reference counterpart)
@@ -512,7 +522,7 @@ class Context:
             raise MassrtError(f"{what} failed ({rc}): {lib().mrt_global_last_error().decode()}")
         self.h = h
         self._images = weakref.WeakSet()  # closed before the context (massrt.h: images first)
-        for k, v in {**env_options(), **(options or {})}.items():
+        for k, v in (options or {}).items():
             self.set_option(k, v)
 
     def set_option(self, name: str, value: int):

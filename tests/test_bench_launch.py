@@ -77,3 +77,19 @@ def test_rehearsal_devices():
 def test_context_options_from_flags():
     assert bench.context_options(_args("--opt", "queues=1", "--opt", "trace_chunk=256")) == \
         {"queues": 1, "trace_chunk": 256}
+
+
+def test_env_options_reach_bench_contexts_only(monkeypatch):
+    """MASSRT_OPTIONS is read by bench.py (context_options), never by
+    massrt.Context itself; --opt overrides it; malformed items name themselves."""
+    import massrt
+
+    monkeypatch.setenv("MASSRT_OPTIONS", "traversal=1, queues=2")
+    assert bench.context_options(_args("--opt", "queues=1")) == {"traversal": 1, "queues": 1}
+    assert massrt.parse_options("a=0x10,b=-1") == {"a": 16, "b": -1}
+    for bad in ("queues", "=3", "queues=x"):
+        with pytest.raises(ValueError, match="not NAME=INTEGER"):
+            massrt.parse_options(bad, "MASSRT_OPTIONS")
+    import inspect
+
+    assert "env_options" not in inspect.getsource(massrt.Context.__init__)

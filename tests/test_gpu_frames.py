@@ -91,6 +91,27 @@ def test_multi_device_context_render_equals_one_device(scene):
     one.close()
 
 
+@pytest.mark.parametrize("devices", [[0, 0, 0], [0]])
+def test_multi_device_shards_accumulate_into_one_host_buffer(scene, devices):
+    """A caller that renders shard 0 then shard 1 of 2 into ONE nonzero host
+    buffer on a multi-device context keeps both shards' sums and every other
+    pixel's starting value (the copy back used to zero the pixels
+    of the shards this call did not render)."""
+    one = _ctx(scene)
+    multi = _ctx(scene, devices=devices)
+    rng = np.random.default_rng(7)
+    start = (rng.random(W * H * 3, dtype=np.float32), rng.integers(0, 1000, W * H).astype(np.uint32))
+    acc1 = (start[0].copy(), start[1].copy())
+    accm = (start[0].copy(), start[1].copy())
+    for s0, si in ((0, 0), (0, 1), (2, 0)):  # shard 1 once, shard 0 twice
+        acc1 = one.render(W, H, s0, 2, seed=4, shard_index=si, shard_count=2, accum=acc1)
+        accm = multi.render(W, H, s0, 2, seed=4, shard_index=si, shard_count=2, accum=accm)
+        assert _same(acc1[0], accm[0]) and _same(acc1[1], accm[1]), (s0, si)
+    assert not _same(accm[0], start[0])
+    multi.close()
+    one.close()
+
+
 def test_multi_device_image_gathers_each_tile_once(scene):
     one = _ctx(scene)
     multi = _ctx(scene, devices=[0, 0, 0])
