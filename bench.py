@@ -508,7 +508,7 @@ def timed_region(world, steps_fn, sync_fn, pg_dev=None):
     return max(per_rank), per_rank
 
 
-def roofline_for(a, scene, cnt, ks, samples_total, elapsed, n_gpus, plan) -> tuple:
+def roofline_for(a, scene, cnt, ks, samples_total, elapsed, n_gpus, plan, trav: int = 0) -> tuple:
     """(roofline of k_trace, roofline_k_shade) from the counting warmup step's
     event counts and the timed steps' HIP-event kernel times."""
     if not (cnt["samples"] > 0 and ks["trace_launches"] > 0):
@@ -526,8 +526,8 @@ def roofline_for(a, scene, cnt, ks, samples_total, elapsed, n_gpus, plan) -> tup
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     import massrt
 
-    # the walk the run used (option traversal): its own profile, profiles/pmc_<scene>_nf.json for the near-first walk
-    trav = int(context_options(a).get("traversal", 0))
+    # the walk the run used (`trav`, the context's tuning): its own profile,
+    # profiles/pmc_<scene>_nf.json for the near-first walk
     stamp = {"scene": scene, "width": a.width, "height": a.height, "spp_per_step": plan["spp_per_step"],
              "src": src_hash(), "n_gpus": n_gpus, "traversal": trav}
     tag = "_nf" if trav else ""
@@ -641,7 +641,8 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
     if timing:
         # ranks mode: this rank's share of the samples and its own launches
         share = samples_total / (world if devices is None else 1)
-        roof, shade = roofline_for(a, scene, cnt, ks, share, elapsed, n_gpus, plan)
+        roof, shade = roofline_for(a, scene, cnt, ks, share, elapsed, n_gpus, plan,
+                                   int(r.ctx.tuning().get("traversal", 0)))
     out = {"scene": scene, "value": round(value, 3), "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps,
            "warmup": warmup, "width": W, "height": H, "spp_per_step": spp, "samples_per_step": W * H * spp,
            "workload": plan["workload"], "scaling": plan["scaling"], "n_gpus": n_gpus,
@@ -709,31 +710,40 @@ def config_lines(a, rank, world, dev, devices) -> dict:
     return out
 
 
-def near_first_lines(a, rank, world, dev, devices, exact: dict) -> dict:
-    """The opt-in near-first walk (option traversal=1, massrt.h) on the same
-    workloads as the exact lines: headline, secondary and config 3. Its hits
-    equal the reference walk's except for rays grazing large triangles
-    (DESIGN.md §4 has the measured rates), so it is reported beside the
-    headline, never as `value`."""
+WALK_NAMES = {0: "reference", 1: "near_first"}
+
+
+def other_walk_lines(a, rank, world, dev, devices, runs: dict) -> dict:
+    """Each workload of the line (headline, secondary, config 3) again with
+    the other walk (massrt.h MRT_TRAVERSAL_*): the default (AUTO) takes the
+    proven near-first walk where it is faster (sphere_grid, cube_field) and
+    the reference's left-first walk elsewhere (mesh_ply, Menger), so the line
+    carries both numbers for every scene. Both walks return the reference's
+    closest hits."""
     import copy
 
-    b = copy.copy(a)
-    b.opt = list(a.opt) + ["traversal=1"]
-    out = {"option": "traversal=1 (MRT_TRAVERSAL_NEAR_FIRST)",
-           "exactness": "same hits as the reference walk on every GPU test frame and on 1.2M adversarial "
-                        "grazing/tangent rays (DESIGN.md §4); not proven exact, so never the headline"}
+    out = {"exactness": "both walks return the reference's closest hits: the reference walk by construction, the "
+                        "near-first walk by the rounding bound of DESIGN.md §4 (slab_check bound checks, GPU parity)"}
     for key, scene, steps, kw in (("headline", a.scene, 2, {}), ("secondary", a.secondary, 2, {}),
                                   ("c3", "cube_field", 1, dict(spp=1024))):
-        if not scene or scene == "none" or (key == "secondary" and scene == a.scene):
+        used = runs.get(key)
+        if not scene or scene == "none" or not used or "value" not in used:
             continue
+        walk = int(used.get("tuning", {}).get("traversal", 0))
+        other = 1 - walk
+        b = copy.copy(a)
+        b.opt = list(a.opt) + [f"traversal={other}"]
         try:
             r = run_scene(b, scene, steps, 1, rank, world, dev, False, devices, **kw)
-            ref = exact.get(key)
-            out[key] = {"scene": scene, "workload": r["workload"], "value": r["value"], "ms_per_step": r["ms_per_step"],
-                        "steps": steps, "of_exact": round(r["value"] / ref, 3) if ref else None,
-                        "traversal": r["tuning"].get("traversal"),
+            got = int(r["tuning"].get("traversal", 0))
+            out[key] = {"scene": scene, "walk_used": WALK_NAMES[walk], "value_used": used["value"],
+                        "other_walk": WALK_NAMES[got], "other_value": r["value"],
+                        "used_over_other": round(used["value"] / r["value"], 3) if r["value"] else None,
+                        "ms_per_step": r["ms_per_step"], "steps": steps,
                         "vnf_fallback_frac": (r["roofline"] or {}).get("vnf_fallback_frac"),
                         "k_trace_avg_launch_ms": ((r["roofline"] or {}).get("k_trace") or {}).get("avg_launch_ms")}
+            if got == walk:
+                out[key]["note"] = "the scene has no near-first trees: one walk only"
         except Exception as e:
             out[key] = {"error": str(e)}
     return out
@@ -800,12 +810,11 @@ def main():
                     dropin[sc] = dropin_run(a, sc, ref)
                 except Exception as e:
                     dropin[sc] = {"error": str(e)}
-    near_first = None
+    walks = None
     if rank == 0 and solo and not a.no_configs:
         configs = config_lines(a, rank, world, dev, devices)
-        exact = {"headline": head["value"], "secondary": sec["value"] if sec else None,
-                 "c3": (configs.get("c3") or {}).get("value")}
-        near_first = near_first_lines(a, rank, world, dev, devices, exact)
+        walks = other_walk_lines(a, rank, world, dev, devices,
+                                 {"headline": head, "secondary": sec, "c3": configs.get("c3")})
     if cpu:
         try:
             c1 = c1_runs(a)
@@ -855,8 +864,9 @@ def main():
             line["config"]["dropin"] = dropin
         if configs:
             line["config"].update(configs)
-        if near_first:
-            line["config"]["near_first"] = near_first
+        if walks:
+            line["config"]["walks"] = walks
+        line["config"]["walk"] = WALK_NAMES.get(int((head.get("tuning") or {}).get("traversal", 0)))
         if head.get("roofline_k_shade"):
             line["roofline_k_shade"] = head["roofline_k_shade"]
         if head.get("gather"):

@@ -298,6 +298,7 @@ pub struct mrt_tuning {
 }
 
 /// Context option "traversal" (ABI v8).
+pub const MRT_TRAVERSAL_AUTO: i64 = -1;
 pub const MRT_TRAVERSAL_REFERENCE: i64 = 0;
 pub const MRT_TRAVERSAL_NEAR_FIRST: i64 = 1;
 

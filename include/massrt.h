@@ -337,9 +337,11 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  *   trace_block       256, 512, 1024  k_trace workgroup beside a treelet
  *   mem_reserve_mb    device memory a render leaves free (default 4096)
  *   gather            MRT_GATHER_* (multi-device contexts)
- *   traversal         MRT_TRAVERSAL_* (default REFERENCE); NEAR_FIRST applies
- *                     to scenes without traversal draws (Volume, Mix alpha)
- *                     and without a treelet, others keep REFERENCE
+ *   traversal         MRT_TRAVERSAL_* (default AUTO: per scene); NEAR_FIRST
+ *                     applies to scenes without traversal draws (Volume, Mix
+ *                     alpha) and without a treelet, others keep REFERENCE
+ *   nf_kappa_log2     -40..-8  NEAR_FIRST: rays whose generic-triangle kappa
+ *                     (nf_bound.h) exceeds 2^v take the reference walk (-8)
  *   trace_nf_batch    -1, 1..64  NEAR_FIRST: finished walks checked together
  *                     once this many lanes wait (-1: the refill threshold)
  * Every render sizes its path pool and results slab to the device memory
@@ -349,18 +351,21 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  * REFERENCE walks the reference's tree left child first (the reference's own
  * sequence of box and primitive tests: bit-exact by construction). NEAR_FIRST
  * walks surface-area-heuristic trees over the same primitives, nearer child
- * first, culling boxes whose entry exceeds the best t by 2^-10, then checks
- * that the reference's walk reaches the hit it found (its innermost reference
- * ancestors pass BoundingBox::hit at that t) and walks the reference's way
- * where it does not. Its hits equal the reference's unless a primitive's
- * computed t undercuts its own box by more than the culling margin, which
- * Moller-Trumbore's t can do for rays nearly parallel to a large triangle;
- * the walk's triangle boxes are thickened against it, and no difference
- * was found in the GPU test frames nor in 1.2M adversarial grazing/tangent
- * rays, but it is not proven. Measured round 4: 1.25x / 1.41x /
- * 1.46x the reference walk on sphere_grid / mesh_ply / cube_field, but 0.56x on
- * Menger (a 4.19M-node TLAS: trace_nf_batch 64 brings it to ~1.0x). Counters
- * (node visits, ...) then count its work. */
+ * first, then checks that the reference's walk reaches the hit it found (its
+ * innermost reference ancestors pass BoundingBox::hit) and walks the
+ * reference's way where it does not. Its boxes are thickened by a proven
+ * bound on how far a primitive's computed hit can lie outside its box (the
+ * reference's own f32 Moller-Trumbore and sphere roots, instance transforms;
+ * DESIGN.md §4), so it meets every hit that can win and its closest hit is
+ * the reference's, t bits and ties included; rays the bound does not cover
+ * take the reference's walk. AUTO (the default) picks NEAR_FIRST unless the
+ * bound has the generic-triangle term (large arbitrary triangles seen by
+ * long camera rays: mesh_ply) or the world is a big instanced one (Menger),
+ * where REFERENCE is faster. Measured round 5 (1080p x 1024 spp per step):
+ * sphere_grid 976 vs 926, cube_field 504 vs 413 Msamples/s; mesh_ply 548 vs
+ * 1148 and Menger 26 vs 50 (hence AUTO). Counters (node visits, ...) count
+ * the walk taken. */
+#define MRT_TRAVERSAL_AUTO (-1)
 #define MRT_TRAVERSAL_REFERENCE 0
 #define MRT_TRAVERSAL_NEAR_FIRST 1
 #define MRT_GATHER_AUTO 0 /* RCCL between distinct devices, peer copies otherwise */

@@ -32,6 +32,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "nf_bound.h"
+
 namespace mrt {
 
 enum : uint32_t { KIND_BOX = 1, KIND_SPHERE = 2, KIND_TRI = 3, KIND_INST = 4, KIND_MODEL = 5, KIND_VOLUME = 6 };
@@ -79,6 +81,9 @@ constexpr uint32_t kTriIdMask = 0x0FFFFFFFu;
 //           record or kNfPop (continue with the stack)
 //   INST / MODEL {id, nf_blas_root, next, 0} {0,0,0,INST|MODEL}
 constexpr uint32_t kNfIdx = 0x0FFFFFFFu;  // index bits of an NF node's children base
+// an NF node's slot1.w: its left / right child is never culled (the subtree
+// of "wild" instances, whose rounding the world margin does not cover; nf_tree.cpp)
+constexpr uint32_t kNfForceL = 0x10000000u, kNfForceR = 0x20000000u;
 constexpr uint32_t kNfPop = 0x0FFFFFFFu;  // "next" of a leaf's last record: pop the stack
 constexpr int kNfExpMin = -100;            // smallest plane step 2^e (products with 1/d stay normal)
 constexpr uint32_t kNfStack = 24u;         // stack entries per lane (LDS): the trees' depth is capped to fit
@@ -175,6 +180,7 @@ struct DevScene {
   const uint32_t* vnf_leaf;    // {reference parent box, order key} pairs per leaf object
   uint32_t vnf_base[4];        // first vnf_leaf entry of spheres, triangles, instances, models
   uint32_t n_vnf;
+  NfBound nfb;                 // the walk's rounding margins (nf_bound.h)
 };
 
 }  // namespace mrt

@@ -86,20 +86,77 @@ void pad_box(Box& b, float rel_extra) {
   for (int k = 0; k < 3; ++k) b.mn[k] = pad(b.mn[k], -1.0f, rel_extra), b.mx[k] = pad(b.mx[k], 1.0f, rel_extra);
 }
 
-// NF triangle boxes are thickened by this fraction of the triangle's extent
-// (object_box): grazing rays, whose computed t can undercut the plane far
-// more than the culling margin, then meet the box before the plane
-constexpr float kTriThick = 0x1p-6f;
+// ---- the rounding bounds (nf_bound.h; DESIGN.md §4 "Why the near-first walk
+// is exact"): u = 2^-24, gamma_n = n u / (1 - n u) ----
+constexpr double kU = 0x1p-24;
+double gam(int n) { return n * kU / (1.0 - n * kU); }
+// a float at or below / above v
+float f_down(double v) {
+  float f = (float)v;
+  if ((double)f > v) f = nextafterf(f, -INFINITY);
+  return f;
+}
+float f_up(double v) {
+  float f = (float)v;
+  if ((double)f < v) f = nextafterf(f, INFINITY);
+  return f;
+}
+double norm3(const double v[3]) { return std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+
+// A triangle's bound on how far its computed hit X = o + t d can lie from the
+// triangle (Triangle::intersect, geom.rs:504-533, as path.h tri_hit computes
+// it): |X - tri| <= a(|d|) L + pad with L = |X - o| and a(|d|) = a0 + a1 |d|;
+// pad (proportional to the triangle's size) is added to its box on the host.
+// k1: generic kappa per unit |d| (the walk requires k1 |d| <= kNfKappaMax).
+struct TriBound {
+  double a0 = 0, a1 = 0, k1 = 0, pad = 0;
+};
+TriBound tri_bound(const float ab[3], const float ac[3]) {
+  const double u = kU;
+  const double dab[3] = {ab[0], ab[1], ab[2]}, dac[3] = {ac[0], ac[1], ac[2]};
+  const double S = norm3(dab) + norm3(dac), M2 = norm3(dab) * norm3(dac);
+  // axis-structured: ab_k == ac_k == 0 — the plane x_k = const; every product
+  // with those zeros is exact, det = d_k n_k up to the two in-plane products'
+  // roundings, and the residual's terms all carry d_k or (o - a)_k
+  for (int k = 0; k < 3; ++k) {
+    if (!(ab[k] == 0.0f && ac[k] == 0.0f)) continue;
+    const int j = (k + 1) % 3, l = (k + 2) % 3;  // n_k = ab_j ac_l - ab_l ac_j (cross, mrt_math.h)
+    const double p1 = dab[j] * dac[l], p2 = dab[l] * dac[j];  // exact
+    const double nk = std::fabs(p1 - p2), n1 = std::fabs(p1) + std::fabs(p2);
+    if (!(nk > 0)) break;  // degenerate: the generic bound
+    const double sl = n1 / nk, sigma = M2 / nk;
+    const double beta = 1.0 - 3.01 * u * sl;
+    if (beta < 0.5) break;
+    const double lambda = (1.0 + 3.01 * u * sl) / ((1.0 - 3.01 * u * sl) * (1.0 - gam(2)));
+    const double kap = u + 19.01 * u * sigma / beta;
+    if (kap > (double)kNfKappaMax) break;
+    TriBound b;
+    b.a0 = (kap + 16.0 * u * sigma * lambda / beta + 2.01 * u) / (1.0 - kap);
+    b.pad = ((1.0001 * kap + 2.01 * u) / (1.0 - kap) + 3.01 * u) * S;
+    return b;
+  }
+  // generic: |det| >= 0.000001f (the reference's own test) bounds the
+  // cancellation: kappa = u + c_g M2 |d|, c_g = 1.0001 * 24u / 0.000001f
+  const double km = 1.01 * (double)kNfKappaMax, cg = 1.0001 * 24.0 * u * 1.0000001e6;
+  TriBound b;
+  b.a0 = 3.01 * u / (1.0 - km);
+  b.a1 = cg * M2 / (1.0 - km);
+  b.k1 = cg * M2;
+  b.pad = ((1.0001 * km + 2.01 * u) / (1.0 - km) + 3.01 * u) * S;
+  return b;
+}
 
 // ---- binned SAH over items ----
 struct Item {
   Box b;
-  uint32_t rec;  // the item's record in the reference stream
+  uint32_t rec;       // the item's record in the reference stream
+  bool wild = false;  // never culled (nf_tree.cpp wild()): the nodes on its path force their child
 };
 struct Node {
   Box b;
   int32_t l = -1, r = -1;
   uint32_t first = 0, count = 0, axis = 0;
+  uint32_t force = 0;  // kNfForceL / kNfForceR: that child is never culled (wild instances)
 };
 struct Tree {
   std::vector<Node> nodes;
@@ -188,6 +245,20 @@ struct Tree {
     nodes[id].l = l, nodes[id].r = r, nodes[id].axis = (uint32_t)axis;
     return id;
   }
+  // every node forces its child whose subtree holds a wild item (the path
+  // from the root to each wild leaf is never culled); returns whether node
+  // n's subtree holds one
+  bool mark_forced(int32_t n) {
+    Node& x = nodes[n];
+    if (x.l < 0) {
+      for (uint32_t i = 0; i < x.count; ++i)
+        if (items[x.first + i].wild) return true;
+      return false;
+    }
+    const bool wl = mark_forced(x.l), wr = mark_forced(x.r);
+    nodes[n].force = (wl ? kNfForceL : 0u) | (wr ? kNfForceR : 0u);
+    return wl || wr;
+  }
 };
 
 struct Builder {
@@ -270,7 +341,7 @@ struct Builder {
     if (!quantize(L.b, R.b, o, ew, q)) return false;
     uint32_t* rec = &w[4 * (size_t)at];
     rec[0] = o[0], rec[1] = o[1], rec[2] = o[2], rec[3] = ew | lsz << 24;
-    rec[4] = q[0], rec[5] = q[1], rec[6] = q[2], rec[7] = kBoxFlag | base;
+    rec[4] = q[0], rec[5] = q[1], rec[6] = q[2], rec[7] = kBoxFlag | n.force | base;
     s.nf_boxes++;
     for (const auto& [c, pos] : {std::pair<const Node*, uint32_t>{&L, base}, {&R, base + lsz}}) {
       if (c->l < 0)
@@ -353,14 +424,36 @@ struct Builder {
     return true;
   }
 
-  Box object_box(uint32_t r) {
+  // ---- boxes and bounds (nf_bound.h) ----
+  std::unordered_map<uint32_t, size_t> region_of;  // reference BLAS region begin -> blas_regions index
+  std::vector<Box> blas_box;                       // each BLAS's NF root box (object space, padded)
+  std::vector<TriBound> blas_bound;                // each BLAS's worst triangle bound (max of a0, a1, k1)
+  TriBound world_tri;                              // world triangles and model BLAS triangles
+  double r_min = INFINITY, r_max = 0;
+  Box sph_box;                                     // the world spheres' union
+  struct InstTerm {
+    double w0, w1, b0, b1, ko;
+  };
+
+  static void grow_bound(TriBound& m, const TriBound& b) {
+    m.a0 = std::max(m.a0, b.a0), m.a1 = std::max(m.a1, b.a1), m.k1 = std::max(m.k1, b.k1);
+  }
+  static void pad_abs(Box& b, double p) {
+    for (int k = 0; k < 3; ++k) b.mn[k] = f_down((double)b.mn[k] - p), b.mx[k] = f_up((double)b.mx[k] + p);
+  }
+
+  // A leaf object's NF box: its geometry, every hit it can return within
+  // the size-proportional pads of its bound (the distance-proportional part
+  // is the walk's margin, nf_bound.h).
+  Box object_box(uint32_t r, TriBound* tb) {
     Box b;
     const uint32_t* q = &w[4 * (size_t)r];
     switch (kind_of(w, r)) {
       case KIND_SPHERE: {
-        const float rad = fabsf(u2f(q[3]));
-        for (int k = 0; k < 3; ++k) b.mn[k] = u2f(q[k]) - rad, b.mx[k] = u2f(q[k]) + rad;
-        pad_box(b, 0x1p-20f);  // the rounded c +- r, and the sphere test's own rounding
+        // the ball, plus the bound's terms proportional to the radius (90.2u |r|)
+        const double rad = std::fabs((double)u2f(q[3])) * (1.0 + 0x1p-17);
+        for (int k = 0; k < 3; ++k) b.mn[k] = f_down(u2f(q[k]) - rad), b.mx[k] = f_up(u2f(q[k]) + rad);
+        pad_box(b, 0.0f);
         break;
       }
       case KIND_TRI: {
@@ -368,55 +461,100 @@ struct Builder {
         b.grow(t.a[0], t.a[1], t.a[2]);
         b.grow(t.b[0], t.b[1], t.b[2]);
         b.grow(t.c[0], t.c[1], t.c[2]);
+        const float ab[3] = {u2f(q[3]), u2f(q[4]), u2f(q[5])}, ac[3] = {u2f(q[8]), u2f(q[9]), u2f(q[10])};
+        const TriBound tbd = tri_bound(ab, ac);
+        if (tb) grow_bound(*tb, tbd);
         pad_box(b, 0.0f);
-        // a slab of kTriThick x the triangle's extent on every side: a ray
-        // grazing the triangle at angle a enters the box h / sin(a) before
-        // the plane, while Moller-Trumbore's t can undercut the plane by
-        // ~dist * eps / sin(a) — the sin(a) cancels, so hits within
-        // ext * kTriThick / (c * eps) of the ray origin (~10^5 x the
-        // triangle's extent) can never be culled
-        {
-          float ext = 0.0f;
-          for (int k = 0; k < 3; ++k) ext = fmaxf(ext, b.mx[k] - b.mn[k]);
-          for (int k = 0; k < 3; ++k) b.mn[k] -= ext * kTriThick, b.mx[k] += ext * kTriThick;
-        }
+        pad_abs(b, tbd.pad);
         break;
       }
       case KIND_INST:
       case KIND_MODEL: {
-        const uint32_t blas = q[1];  // the reference BLAS root record (a box)
-        Box ob;
-        if (is_box(w, blas)) {
-          const uint32_t* p = &w[4 * (size_t)blas];
-          ob.grow(u2f(p[0]), u2f(p[1]), u2f(p[2]));
-          ob.grow(u2f(p[3]), u2f(p[4]), u2f(p[5]));
-        } else {
-          ob.grow(-INFINITY, -INFINITY, -INFINITY);
-          ob.grow(INFINITY, INFINITY, INFINITY);
-        }
-        if (kind_of(w, r) == KIND_MODEL) {
-          b = ob;
-          pad_box(b, 0.0f);
+        auto it = region_of.find(q[1]);  // the reference BLAS region it enters
+        if (it == region_of.end()) {
+          b.grow(-INFINITY, -INFINITY, -INFINITY);
+          b.grow(INFINITY, INFINITY, INFINITY);
           break;
         }
+        const Box& ob = blas_box[it->second];
+        if (kind_of(w, r) == KIND_MODEL) {
+          b = ob;
+          break;
+        }
+        // the hull of the transformed corners, in double (each product of
+        // two floats exact, the sum's rounding added) and rounded outward
         const float* f = d.instances[q[0]].fwd;  // column-major 4x4 (M4::transform)
         for (int c = 0; c < 8; ++c) {
-          const float x = c & 1 ? ob.mx[0] : ob.mn[0], y = c & 2 ? ob.mx[1] : ob.mn[1], z = c & 4 ? ob.mx[2] : ob.mn[2];
-          b.grow(((f[0] * x + f[4] * y) + f[8] * z) + f[12], ((f[1] * x + f[5] * y) + f[9] * z) + f[13],
-                 ((f[2] * x + f[6] * y) + f[10] * z) + f[14]);
+          const double x = c & 1 ? ob.mx[0] : ob.mn[0], y = c & 2 ? ob.mx[1] : ob.mn[1], z = c & 4 ? ob.mx[2] : ob.mn[2];
+          for (int k = 0; k < 3; ++k) {
+            const double t0 = (double)f[k] * x, t1 = (double)f[4 + k] * y, t2 = (double)f[8 + k] * z, t3 = f[12 + k];
+            const double v = ((t0 + t1) + t2) + t3;
+            const double e = 0x1p-50 * (std::fabs(t0) + std::fabs(t1) + std::fabs(t2) + std::fabs(t3));
+            b.mn[k] = std::min(b.mn[k], f_down(v - e)), b.mx[k] = std::max(b.mx[k], f_up(v + e));
+          }
         }
-        // the object-space walk runs on the inverse-transformed ray: its
-        // rounding moves hits by a few ulps of the transform's magnitudes
-        float mag = 0.0f;
-        for (int k = 0; k < 3; ++k) mag = fmaxf(mag, fmaxf(fabsf(b.mn[k]), fabsf(b.mx[k])));
-        pad_box(b, 0x1p-16f);
-        for (int k = 0; k < 3; ++k) b.mn[k] -= mag * 0x1p-18f, b.mx[k] += mag * 0x1p-18f;
         break;
       }
       default:
         break;
     }
     return b;
+  }
+
+  // The world-space terms an instance's object-space rounding contributes
+  // (DESIGN.md §4): F = fwd, G = inv (the stored f32 matrices), the object
+  // ray RN(G o), RN(G d) and the hit mapped back by F.
+  InstTerm inst_term(uint32_t id, const TriBound& ob) const {
+    const float* F = d.instances[id].fwd;
+    const float* G = d.instances[id].inv;
+    double nf = 0, ng = 0, psi = 0, gt = 0, ft = 0;
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) {
+        nf += (double)F[4 * c + r] * F[4 * c + r];
+        ng += (double)G[4 * c + r] * G[4 * c + r];
+        double m = 0;  // (F_L G_L)_rc
+        for (int k = 0; k < 3; ++k) m += (double)F[4 * k + r] * G[4 * c + k];
+        m -= r == c ? 1.0 : 0.0;
+        psi += m * m;
+      }
+    nf = std::sqrt(nf), ng = std::sqrt(ng), psi = std::sqrt(psi) + 0x1p-48 * nf * ng;
+    double pt = 0;
+    for (int r = 0; r < 3; ++r) {
+      double v = F[12 + r];
+      for (int k = 0; k < 3; ++k) v += (double)F[4 * k + r] * G[12 + k];
+      pt += v * v;
+      gt += (double)G[12 + r] * G[12 + r];
+      ft += (double)F[12 + r] * F[12 + r];
+    }
+    pt = std::sqrt(pt) + 0x1p-48 * (nf * std::sqrt(gt) + std::sqrt(ft));
+    gt = std::sqrt(gt);
+    const double cond = nf * ng, g3 = gam(3), g4 = gam(4);
+    InstTerm m;
+    m.w0 = cond * (1 + g3) * ob.a0 + psi + g3 * cond;
+    m.w1 = cond * (1 + g3) * (1 + g3) * ob.a1 * ng;
+    m.b1 = psi + g4 * cond;
+    m.b0 = pt + g4 * nf * gt;
+    m.ko = ob.k1 * ng * (1 + g3);
+    return m;
+  }
+  // a wild instance: its terms would dominate the world margin; the walk
+  // never culls it (and its subtree) instead
+  static bool wild(const InstTerm& m) { return m.w0 > 0x1p-14 || m.w1 > 0x1p-14 || m.b1 > 0x1p-14; }
+
+  // vnf_leaf slot of a leaf object's record
+  uint32_t vnf_slot(uint32_t r) const {
+    const uint32_t* q = &w[4 * (size_t)r];
+    switch (kind_of(w, r)) {
+      case KIND_SPHERE: return s.vnf_base[VNF_SPHERE] + q[4];
+      case KIND_TRI: return s.vnf_base[VNF_TRI] + (q[6] & kTriIdMask);
+      case KIND_INST: return s.vnf_base[VNF_INST] + q[0];
+      default: return s.vnf_base[VNF_MODEL] + q[0];
+    }
+  }
+  void keep_box(uint32_t r, const Box& b) {
+    if (!s.keep_nf_boxes) return;
+    float* p = &s.nf_leaf_box[6 * (size_t)vnf_slot(r)];
+    for (int k = 0; k < 3; ++k) p[k] = b.mn[k], p[3 + k] = b.mx[k];
   }
 
   bool run() {
@@ -432,31 +570,136 @@ struct Builder {
     if (!ref_order(s.world_begin, true, world_objs)) return true;
     if (world_objs.empty()) return (s.nf_note = "an empty world", true);
     std::vector<std::vector<uint32_t>> blas_objs(s.blas_regions.size());
-    for (size_t k = 0; k < s.blas_regions.size(); ++k)
+    if (s.keep_nf_boxes) {
+      s.nf_leaf_box.assign(3 * s.vnf_leaf.size(), NAN);
+      s.nf_inst_wild.assign(d.n_instances, 0);
+    }
+    for (size_t k = 0; k < s.blas_regions.size(); ++k) {
+      region_of[s.blas_regions[k].begin] = k;
       if (!ref_order(s.blas_regions[k].begin, false, blas_objs[k])) return true;
+    }
+    // which BLAS regions models / instances enter (world objects)
+    std::vector<uint8_t> by_model(s.blas_regions.size(), 0), by_inst(s.blas_regions.size(), 0);
+    for (uint32_t r : world_objs) {
+      const uint32_t kd = kind_of(w, r);
+      if (kd != KIND_INST && kd != KIND_MODEL) continue;
+      auto it = region_of.find(w[4 * (size_t)r + 1]);
+      if (it != region_of.end()) (kd == KIND_MODEL ? by_model : by_inst)[it->second] = 1;
+    }
     // trees; stack entries the walk may need: a far child per internal level
     // of the world tree, an instance's successor and its return marker, a far
     // child per BLAS level — kept within kNfStack by capping the depth (median
     // splits at the cap's edge): the BLAS trees first, leaving the world tree
-    // at least the levels a balanced tree over its objects needs
-    Tree world;
-    for (uint32_t r : world_objs) world.items.push_back({object_box(r), r});
+    // at least the levels a balanced tree over its objects needs (and one for
+    // the wild instances' subtree)
     const uint32_t has_blas = s.blas_regions.empty() ? 0 : 2;
     std::vector<Tree> blas(s.blas_regions.size());
+    blas_box.assign(s.blas_regions.size(), Box{});
+    blas_bound.assign(s.blas_regions.size(), TriBound{});
     uint32_t blas_depth = 0;
-    const uint32_t world_min = Tree::min_levels((uint32_t)world.items.size());
+    const uint32_t world_min = Tree::min_levels((uint32_t)world_objs.size());
     if (world_min + has_blas > kNfStack) return (s.nf_note = "too many world objects for the walk's stack", true);
     for (size_t k = 0; k < blas.size(); ++k) {
-      for (uint32_t r : blas_objs[k]) blas[k].items.push_back({object_box(r), r});
+      for (uint32_t r : blas_objs[k]) {
+        blas[k].items.push_back({object_box(r, &blas_bound[k]), r});
+        keep_box(r, blas[k].items.back().b);
+      }
       if (blas[k].items.empty()) continue;
       blas[k].max_depth = kNfStack - 2 - world_min;
       blas[k].build(0, (uint32_t)blas[k].items.size(), 0);
       blas_depth = std::max(blas_depth, blas[k].depth);
+      blas_box[k] = blas[k].nodes[0].b;
+      if (by_model[k]) grow_bound(world_tri, blas_bound[k]);
     }
+    // the world's items: wild instances first
+    Tree world;
+    NfBound& B = s.nfb;
+    B = NfBound{};
+    double aw0 = 0, aw1 = 0, bw0 = 0, bw1 = 0, ko1 = 0, ao0 = 0, ao1 = 0, orad = 0;
+    std::vector<Item> wild_items, items;
+    Box gen_box;  // the world boxes of generic triangles (world, model or instanced): the a1 term's ball
+    for (uint32_t r : world_objs) {
+      const uint32_t kd = kind_of(w, r);
+      TriBound tb;
+      const Box b = object_box(r, kd == KIND_TRI ? &tb : nullptr);
+      keep_box(r, b);
+      if (kd == KIND_TRI) grow_bound(world_tri, tb);
+      bool generic = tb.a1 > 0;
+      if (kd == KIND_INST || kd == KIND_MODEL) {
+        auto it = region_of.find(w[4 * (size_t)r + 1]);
+        generic = it != region_of.end() && blas_bound[it->second].a1 > 0;
+      }
+      if (kd == KIND_SPHERE) {
+        const double rad = std::fabs((double)u2f(w[4 * (size_t)r + 3]));
+        r_min = std::min(r_min, rad), r_max = std::max(r_max, rad);
+        Box sb;
+        for (int k = 0; k < 3; ++k) sb.mn[k] = f_down(u2f(w[4 * (size_t)r + k]) - rad), sb.mx[k] = f_up(u2f(w[4 * (size_t)r + k]) + rad);
+        sph_box.grow(sb);
+      }
+      if (kd == KIND_INST) {
+        auto it = region_of.find(w[4 * (size_t)r + 1]);
+        const TriBound ob = it == region_of.end() ? TriBound{} : blas_bound[it->second];
+        const InstTerm m = inst_term(w[4 * (size_t)r], ob);
+        ko1 = std::max(ko1, m.ko);
+        if (it != region_of.end()) {
+          const Box& bb = blas_box[it->second];
+          for (int c = 0; c < 8; ++c) {
+            const double x = c & 1 ? bb.mx[0] : bb.mn[0], y = c & 2 ? bb.mx[1] : bb.mn[1], z = c & 4 ? bb.mx[2] : bb.mn[2];
+            orad = std::max(orad, std::sqrt(x * x + y * y + z * z));
+          }
+          ao0 = std::max(ao0, ob.a0), ao1 = std::max(ao1, ob.a1);
+        }
+        if (wild(m)) {
+          wild_items.push_back({b, r, true});
+          s.nf_wild++;
+          if (s.keep_nf_boxes) s.nf_inst_wild[w[4 * (size_t)r]] = 1;
+          continue;
+        }
+        aw0 = std::max(aw0, m.w0), aw1 = std::max(aw1, m.w1), bw0 = std::max(bw0, m.b0), bw1 = std::max(bw1, m.b1);
+      }
+      if (generic) gen_box.grow(b);
+      items.push_back({b, r});
+    }
+    aw0 = std::max(aw0, world_tri.a0), aw1 = std::max(aw1, world_tri.a1);
+    if (r_min < 0x1p-60) return (s.nf_note = "a sphere too small for the walk's rounding bound", true);
+    world.items = items;
+    world.items.insert(world.items.end(), wild_items.begin(), wild_items.end());
     world.max_depth = kNfStack - (has_blas ? 2 + blas_depth : 0);
     world.build(0, (uint32_t)world.items.size(), 0);
+    if (!wild_items.empty()) world.mark_forced(0);
     s.nf_stack_need = world.depth + (has_blas ? 2 + blas_depth : 0);
     if (s.nf_stack_need > kNfStack) return (s.nf_note = "trees deeper than the walk's stack", true);
+    // the constants (rounded up) of nf_bound.h
+    auto ball = [](const Box& b, float c[3], float& rr) {
+      double r2 = 0;
+      for (int k = 0; k < 3; ++k) {
+        const double m = 0.5 * ((double)b.mn[k] + (double)b.mx[k]);
+        c[k] = (float)m;
+        const double e = std::max(std::fabs((double)b.mx[k] - c[k]), std::fabs(c[k] - (double)b.mn[k]));
+        r2 += e * e;
+      }
+      rr = f_up(std::sqrt(r2) * (1 + 0x1p-40));
+    };
+    // the a0 term's cap: a ball over the objects the world margin covers (the
+    // wild ones are never culled)
+    Box wb;
+    for (const Item& it : items) wb.grow(it.b);
+    if (items.empty()) wb = world.nodes[0].b;
+    for (int k = 0; k < 3; ++k)
+      if (!(std::fabs(wb.mn[k]) < INFINITY && std::fabs(wb.mx[k]) < INFINITY))
+        return (s.nf_note = "a box the node format cannot hold (not finite)", true);
+    ball(wb, B.wc, B.wr);
+    if (aw1 > 0) ball(gen_box, B.gc, B.gr);
+    B.aw0 = f_up(aw0), B.aw1 = f_up(aw1), B.bw0 = f_up(bw0 + 0x1p-90), B.bw1 = f_up(bw1);
+    B.kw1 = f_up(world_tri.k1), B.ko1 = f_up(ko1);
+    B.ao0 = f_up(ao0), B.ao1 = f_up(ao1), B.orad = f_up(orad);
+    B.kmax = kNfKappaMax;
+    if (r_max > 0) {
+      ball(sph_box, B.sc, B.sr);
+      B.s51 = f_up(51.2 * kU / r_min), B.s28 = f_up(27.8 * kU), B.s130 = f_up(130.2 * kU), B.s11 = f_up(11.2 * kU * r_max);
+    } else {
+      B.sr = -1.0f;
+    }
     s.nf_world = emit(world);
     if (s.nf_world == ~0u) return (s.nf_note = "a box the node format cannot hold (not finite)", true);
     for (size_t k = 0; k < blas.size(); ++k) {
@@ -485,6 +728,7 @@ bool build_nf_trees(const mrt_scene_desc& d, HostScene& s, std::string& err) {
   if (!s.nf_ok) {  // no NF trees: drop whatever was appended
     s.slots.resize(keep);
     s.nf_boxes = 0;
+    s.nf_wild = 0;
     s.vnf_leaf.clear();
   }
   return ok;

@@ -424,6 +424,8 @@ struct Trav {
   PathRng rng;   // the ray's stream, for scenes whose traversal draws (RNG variants only)
   uint32_t sp;   // near-first walk: stack entries in use (kExactMode: the reference's walk)
   float t2;      // near-first walk: the smallest t of the other hits it met (nf_finish)
+  NfLine nfl;    // near-first walk: the current space's rounding margin, for t <= cull(best) (nf_bound.h nf_line)
+  float nl;      // near-first walk: the current node's hits have t <= nl (its box's exit; +inf: unknown)
   bool done;
 #ifdef MRT_DEBUG_BOUNDS
   uint32_t steps;
@@ -575,6 +577,8 @@ MRT_DEV void trav_end_index(const TravIn& in, Trav& t) {
   t.ret = kNoRet;
 }
 
+MRT_DEV void nf_start(const TravIn& in, Trav& t);  // the near-first walk's start (below)
+
 // Start ray `ray` of the pool (World::intersect(ray, in.tmin, tmax)).
 template <bool RNG = false, bool LDS = false>
 MRT_DEV void trav_init(const TravIn& in, Trav& t, uint32_t ray, float tmax, uint32_t start = 0xFFFFFFFFu) {
@@ -596,6 +600,7 @@ MRT_DEV void trav_init(const TravIn& in, Trav& t, uint32_t ray, float tmax, uint
 #ifdef MRT_DEBUG_BOUNDS
   t.steps = 0;
 #endif
+  if (start != 0xFFFFFFFFu) nf_start(in, t);
   trav_fetch<LDS>(in, t);
 }
 
@@ -721,9 +726,12 @@ MRT_DEV void trav_prim(const TravIn& in, Trav& t, LocalCounters& lc) {
 // hit with the reference's tie rule, then checks that the reference's
 // left-first walk reaches that hit; if not it walks again the reference's
 // way (sp = kExactMode: trav_box_index / trav_prim_index on the reference
-// stream, the exact kernel's steps). Boxes are culled at best * (1 + 2^-10):
-// a primitive whose computed t undercuts its box's computed entry by less
-// than that is still found.
+// stream, the exact kernel's steps). Boxes are culled at cull(best) = best *
+// (1 + 2^-10), each thickened by rho (nf_bound.h): a bound, proven for the
+// reference's own f32 arithmetic, on how far a primitive's computed hit can
+// lie outside its box — so the walk meets every primitive whose computed t is
+// at most cull(best). Rays the bound does not cover (a
+// generic triangle's kappa above kNfKappaMax) take the reference's walk.
 constexpr uint32_t kExactMode = kExactModeInit;
 constexpr uint32_t kNfDone = 0xFFFEu;     // Trav::sp: the near-first walk is over, its hit not yet checked
 constexpr uint32_t kNfRet = 0x80000000u;  // stack marker: leave the BLAS (back to the world ray)
@@ -736,18 +744,43 @@ MRT_DEV void nf_push(const NfStack& k, Trav& t, uint32_t v) {
   k.p[t.sp * k.stride] = v;
   t.sp += 1;  // the builder bounds the depth (nf_stack_need <= kNfStack)
 }
+MRT_DEV float nf_cull(float best) { return fmaf(fabsf(best), 0x1p-10f, best); }
+// t.nfc: the rounding margin's coefficients (nf_bound.h) of the space being
+// walked — set when the walk enters a space; nf_rho_at turns them into how
+// far a node's boxes are thickened (trav_box_index_nf)
+MRT_DEV void nf_margin(const TravIn& in, Trav& t) {
+  const bool obj = t.ret != kNoRet && (t.ret & kRetInstance);
+  const NfCoef c = obj ? nf_coef_object(in.S.nfb, t.r.o, t.r.a.b) : nf_coef_world(in.S.nfb, t.r.o, t.r.a.b);
+  t.nfl = nf_line(in.S.nfb, c, nf_cull(t.best));
+}
+// the walk starts at the NF world tree (trav_init): rays its bound does not
+// cover take the reference's walk instead
+MRT_DEV void nf_start(const TravIn& in, Trav& t) {
+  if (nf_ray_ok(in.S.nfb, t.r.a.b)) {
+    nf_margin(in, t);
+    t.nl = INFINITY;
+  } else {
+    t.i = in.world_begin;
+    t.sp = kExactModeInit;
+  }
+}
 // next record from the stack; false: the walk is over
 MRT_DEV bool nf_pop(const TravIn& in, const NfStack& k, Trav& t) {
   for (;;) {
     if (t.sp == 0) return false;
     t.sp -= 1;
+    t.nl = INFINITY;  // a popped node's exit is not kept (LDS: the stack's words are the walk's occupancy limit)
     const uint32_t v = k.p[t.sp * k.stride];
     if (v != kNfRet) {
       t.i = v;
       return true;
     }
-    if (t.ret & kRetInstance) t.r = world_ray(in, t.ray);  // a model shares the world ray
+    const bool inst = (t.ret & kRetInstance) != 0;
     t.ret = kNoRet;
+    if (inst) {  // a model shares the world ray (and its margin)
+      t.r = world_ray(in, t.ray);
+      nf_margin(in, t);
+    }
   }
 }
 MRT_DEV uint32_t vnf_entry(const DevScene& S, uint32_t base, uint32_t id, uint32_t word) {
@@ -773,7 +806,6 @@ MRT_DEV bool nf_better(const TravIn& in, const Trav& t, float th, uint32_t prim)
   if (t.prim == kRefNone) return true;
   return nf_key(in, prim, t.ret) > nf_key(in, t.prim, t.hit_ret);
 }
-MRT_DEV float nf_cull(float best) { return fmaf(fabsf(best), 0x1p-10f, best); }
 // a hit at th (<= the culling bound): the new best, or one of the other hits (t2)
 MRT_DEV void nf_hit(const TravIn& in, Trav& t, float th, uint32_t prim) {
   if (th <= t.best && nf_better(in, t, th, prim)) {
@@ -781,6 +813,7 @@ MRT_DEV void nf_hit(const TravIn& in, Trav& t, float th, uint32_t prim) {
     t.best = th;
     t.prim = prim;
     t.hit_ret = t.ret;
+    t.nfl.rcb = nf_rho_node(t.nfl, nf_cull(th));  // a nearer bound: a smaller cap (the line stays valid below it)
   } else {
     t.t2 = fminf(t.t2, th);
   }
@@ -853,15 +886,18 @@ MRT_DEV void nf_finish(const TravIn& in, Trav& t, LocalCounters& lc) {
 }
 
 // Both children's boxes of an NF node (layout.h NF NODE) against [tmin,
-// tmax]: hit[c] unless the box is certainly missed, ent[c] its entry t. Fast
-// rays: plane t = q * (2^e * y) + (o * y - oy) — 2^e * y is exact, so the
-// error against (plane - o_ray) / d adds the node's |o * y - oy| term to the
-// early decision's margin (box_hit_any) — and only a certain miss counts as
+// tmax], each thickened by rho = nfm (nf_bound.h): hit[c] unless the box is
+// certainly missed, ent[c] its entry t. Fast rays: plane t = q * (2^e * y) +
+// (o * y - oy) -/+ rho * y — 2^e * y is exact, so the error against (plane -/+
+// rho - o_ray) / d adds the node's |o * y - oy -/+ rho * y| term to the early
+// decision's margin (box_hit_any; rho carries a 2^-20 excess for the
+// rounding of rho * y against rho / d) — and only a certain miss counts as
 // one: the walk's boxes may be loose (its hits are checked against the
 // reference tree), never tight. Other rays: the exact test on the decoded
-// planes, each widened by an ulp.
-MRT_DEV void nf_node_test(const uint4& s0, const uint4& s1, const TRay& r, float tmin, float tmax, bool hit[2],
-                          float ent[2]) {
+// planes moved out by rho and widened by an ulp. A child whose force bit is
+// set (kNfForceL/R) is never culled.
+MRT_DEV void nf_node_test(const uint4& s0, const uint4& s1, const TRay& r, float tmin, float tmax, float nfm, bool hit[2],
+                          float ent[2], float ex[2]) {
   const V3 o{u2f(s0.x), u2f(s0.y), u2f(s0.z)};
   const V3 sc{__uint_as_float((s0.w & 0xFFu) << 23), __uint_as_float(((s0.w >> 8) & 0xFFu) << 23),
               __uint_as_float(((s0.w >> 16) & 0xFFu) << 23)};
@@ -870,16 +906,27 @@ MRT_DEV void nf_node_test(const uint4& s0, const uint4& s1, const TRay& r, float
   if (tray_fast(r)) {
     const float ax = sc.x * r.yx, ay = sc.y * r.yy, az = sc.z * r.yz;
     const float bx = fmaf(o.x, r.yx, -r.oyx), by = fmaf(o.y, r.yy, -r.oyy), bz = fmaf(o.z, r.yz, -r.oyz);
-    const float mabs = fmaf(vmax3(fabsf(bx), fabsf(by), fabsf(bz)), 0x1p-20f, fabsf(r.om));
+#ifdef MRT_NF_YMAX  // experiment: the thickening as one t margin rho * 2 max|y| per child
+    const float lbx = bx, lby = by, lbz = bz, hbx = bx, hby = by, hbz = bz;
+    const float mabs = fmaf(vmax3(fabsf(bx), fabsf(by), fabsf(bz)), 0x1p-20f, fabsf(r.om)) +
+                       nfm * (2.0f * vmax3(fabsf(r.yx), fabsf(r.yy), fabsf(r.yz)) * (1.0f + 0x1p-20f));
+#else
+    const float lbx = fmaf(-nfm, r.yx, bx), lby = fmaf(-nfm, r.yy, by), lbz = fmaf(-nfm, r.yz, bz);
+    const float hbx = fmaf(nfm, r.yx, bx), hby = fmaf(nfm, r.yy, by), hbz = fmaf(nfm, r.yz, bz);
+    const float mabs = fmaf(vmax1(vmax3(fabsf(lbx), fabsf(lby), fabsf(lbz)), vmax3(fabsf(hbx), fabsf(hby), fabsf(hbz))),
+                            0x1p-20f, fabsf(r.om));
+#endif
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int b = 6 * c;
-      const float lx = fmaf(q(b), ax, bx), ly = fmaf(q(b + 1), ay, by), lz = fmaf(q(b + 2), az, bz);
-      const float hx = fmaf(q(b + 3), ax, bx), hy = fmaf(q(b + 4), ay, by), hz = fmaf(q(b + 5), az, bz);
+      const float lx = fmaf(q(b), ax, lbx), ly = fmaf(q(b + 1), ay, lby), lz = fmaf(q(b + 2), az, lbz);
+      const float hx = fmaf(q(b + 3), ax, hbx), hy = fmaf(q(b + 4), ay, hby), hz = fmaf(q(b + 5), az, hbz);
       const float t0 = vmax3(vmin1(lx, hx), vmin1(ly, hy), vmax1(vmin1(lz, hz), tmin));
       const float t1 = vmin3(vmax1(lx, hx), vmax1(ly, hy), vmin1(vmax1(lz, hz), tmax));
-      hit[c] = !(t0 - t1 > fmaf(fabsf(t0) + fabsf(t1), 0x1p-19f, mabs));
+      const float m = fmaf(fabsf(t0) + fabsf(t1), 0x1p-19f, mabs);
+      hit[c] = !(t0 - t1 > m) || (s1.w & (kNfForceL << c));
       ent[c] = t0;
+      ex[c] = fmaf(m, 2.0f, t1);  // every hit in the thickened box has t <= this (m covers t1's error and this rounding)
     }
     return;
   }
@@ -887,11 +934,11 @@ MRT_DEV void nf_node_test(const uint4& s0, const uint4& s1, const TRay& r, float
   for (int c = 0; c < 2; ++c) {
     const int b = 6 * c;
     auto lo = [&](float qq, float s, float org) {
-      const float p = fmaf(qq, s, org);
+      const float p = fmaf(qq, s, org) - nfm;
       return p - fmaf(fabsf(p), 0x1p-23f, 0x1p-140f);
     };
     auto hi = [&](float qq, float s, float org) {
-      const float p = fmaf(qq, s, org);
+      const float p = fmaf(qq, s, org) + nfm;
       return p + fmaf(fabsf(p), 0x1p-23f, 0x1p-140f);
     };
     const V3 mn{lo(q(b), sc.x, o.x), lo(q(b + 1), sc.y, o.y), lo(q(b + 2), sc.z, o.z)};
@@ -899,8 +946,9 @@ MRT_DEV void nf_node_test(const uint4& s0, const uint4& s1, const TRay& r, float
     const V3 a = (mn - r.o) / r.d, bb = (mx - r.o) / r.d;  // IEEE quotients (the planes may lie outside the qfast domain)
     const float t0 = vmax3(vmin1(a.x, bb.x), vmin1(a.y, bb.y), vmax1(vmin1(a.z, bb.z), tmin));
     const float t1 = vmin3(vmax1(a.x, bb.x), vmax1(a.y, bb.y), vmin1(vmax1(a.z, bb.z), tmax));
-    hit[c] = !(t1 < t0);
+    hit[c] = !(t1 < t0) || (s1.w & (kNfForceL << c));
     ent[c] = 0.0f;  // left first
+    ex[c] = INFINITY;
   }
 }
 
@@ -911,15 +959,20 @@ template <bool COUNT>
 MRT_DEV void trav_box_index_nf(const TravIn& in, const NfStack& k, Trav& t, LocalCounters& lc) {
   if (COUNT) lc.node_visits += 2;
   bool h[2];
-  float e[2];
-  nf_node_test(t.s0, t.s1, t.r, in.tmin, nf_cull(t.best), h, e);
+  float e[2], x[2];
+  // the hits this node must keep have t <= min(cull(best), nl)
+  const float cb = nf_cull(t.best);
+  const float rho = nf_rho_node(t.nfl, fminf(cb, t.nl));
+  nf_node_test(t.s0, t.s1, t.r, in.tmin, cb, rho, h, e, x);
   const uint32_t base = t.s1.w & kNfIdx, right = base + (t.s0.w >> 24);
   if (h[0] && h[1]) {
     const bool lfirst = !(e[1] < e[0]);
     nf_push(k, t, lfirst ? right : base);
     t.i = lfirst ? base : right;
+    t.nl = lfirst ? x[0] : x[1];
   } else if (h[0] || h[1]) {
     t.i = h[0] ? base : right;
+    t.nl = h[0] ? x[0] : x[1];
   } else if (!nf_pop(in, k, t)) {
     nf_over(t);
   }
@@ -959,6 +1012,7 @@ MRT_DEV void trav_prim_index_nf(const TravIn& in, const NfStack& k, Trav& t, Loc
       load_m12(S.inst_inv + (size_t)MRT_IDX(S, s0.x, S.n_inst, 8) * 12, c0, c1, c2, c3);
       t.r = make_tray(xform(c0, c1, c2, c3, t.r.o, 1.0f), xform(c0, c1, c2, c3, t.r.d, 0.0f), S.fast_ok);
       t.ret = (t.i + 2) | kRetInstance;
+      nf_margin(in, t);  // the object space's margin
     } else {
       if (COUNT) lc.model_entries++;
       t.ret = t.i + 2;

@@ -269,7 +269,7 @@ constexpr uint32_t kStashQuads = 4;      // float4s per lane of the world-ray st
 // dynamic shared memory), the winner checked against the reference tree,
 // rays that fail the check walked again the reference's way.
 template <bool COUNT, bool LDS, uint32_t ALPHA, bool RNG, int BLK, bool NF = false>
-__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(NF ? (COUNT ? 1 : 6) : (ALPHA == 0 && !RNG && !COUNT ? 8 : 1)))) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
+__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(NF ? (COUNT ? 1 : 5) : (ALPHA == 0 && !RNG && !COUNT ? 8 : 1)))) void k_trace(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl, uint32_t cur,
                                                   DevCounters* cnt, float tmin, float tmax, TraceTune tune) {
   static_assert(!NF || (!LDS && !RNG), "the near-first walk has no treelet and no traversal draws");
   constexpr int R = 1;
@@ -1021,8 +1021,9 @@ enum OptId {
   OPT_TREELET_KB,        // LDS treelet per workgroup, KiB (0: none); applies at the next upload
   OPT_TRACE_BLOCK,       // k_trace workgroup size beside a treelet: 256, 512 or 1024
   OPT_MEM_RESERVE_MB,    // device memory a render leaves free when it sizes the pool and results slab
-  OPT_TRAVERSAL,         // 0: the reference's left-first walk; 1: the verified near-first walk (MRT_TRAVERSAL_*)
+  OPT_TRAVERSAL,         // 0: the reference's left-first walk; 1: the verified near-first walk; -1: per scene (MRT_TRAVERSAL_*)
   OPT_TRACE_NF_BATCH,    // near-first walk: lanes whose walks are over wait for this many to check their hits together (-1: = refill)
+  OPT_NF_KAPPA_LOG2,     // near-first walk: rays whose generic-triangle kappa exceeds 2^v take the reference walk (-8: every ray the bound covers)
   kNumOpts
 };
 struct OptDef {
@@ -1045,8 +1046,9 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"treelet_kb", 0, 0, 150},
     {"trace_block", 256, 256, 1024},
     {"mem_reserve_mb", 4096, 0, 1 << 20},
-    {"traversal", 0, 0, 1},
+    {"traversal", -1, -1, 1},
     {"trace_nf_batch", -1, -1, 64},
+    {"nf_kappa_log2", -8, -40, -8},
 };
 int opt_find(const char* name) {
   if (!name) return -1;
@@ -1129,6 +1131,7 @@ struct mrt_ctx {
   int shade_wpe = 8;               // k_shade register budget: 8 or 7 waves/SIMD (option "shade_waves")
   uint32_t tl_boxes = 0;           // box records in the treelet
   bool scene_nf = false;           // the scene has verified near-first trees (nf_tree.cpp)
+  bool scene_nf_gen = false;       // their rounding margin has a generic-triangle term (nf_bound.h aw1 / ko1)
   std::string nf_note;             // why it has none
   bool use_nf = false;             // k_trace walks them (option "traversal", the scene, no treelet)
   // LDS treelet: off by default. Measured: it removes the
@@ -1242,7 +1245,14 @@ void apply_options(mrt_ctx* c) {
   const int64_t* o = c->opt;
   const bool inst = c->scene_instances > 1000, big = c->scene_big;
   c->treelet_kb = (uint32_t)o[OPT_TREELET_KB];
-  c->use_nf = o[OPT_TRAVERSAL] == MRT_TRAVERSAL_NEAR_FIRST && c->scene_nf && !c->trace_lds && !c->scene_rng;
+  // traversal -1 (per scene): the near-first walk unless its margin has the
+  // generic-triangle term (mesh_ply 548 vs 1148 Msamples/s: |det| >= 1e-6
+  // bounds Moller-Trumbore's rounding only loosely for camera rays, whose
+  // |d| is ~9) or the world is a big instanced one (Menger 25.7 / 45.9 at
+  // trace_nf_batch 64 vs 50.0); profiles/r5_walk_ab/
+  const bool nf_rule = !c->scene_nf_gen && !(inst && big);
+  c->use_nf = (o[OPT_TRAVERSAL] == MRT_TRAVERSAL_NEAR_FIRST || (o[OPT_TRAVERSAL] < 0 && nf_rule)) && c->scene_nf &&
+              !c->trace_lds && !c->scene_rng;
   const bool nf = c->use_nf, big_solid = big && !inst;
   c->n_queues = (int)o[OPT_QUEUES];
   c->pool_paths = (size_t)o[OPT_POOL_PATHS];
@@ -1263,6 +1273,7 @@ void apply_options(mrt_ctx* c) {
   c->mem_reserve = (size_t)o[OPT_MEM_RESERVE_MB] << 20;
   if (c->wgs_per_cu != (uint32_t)o[OPT_TRACE_WGS_PER_CU]) c->grids.clear();
   c->wgs_per_cu = (uint32_t)o[OPT_TRACE_WGS_PER_CU];
+  c->S.nfb.kmax = ldexpf(1.0f, (int)o[OPT_NF_KAPPA_LOG2]);
 }
 
 // Validates and stores option `id`; the caller re-derives (apply_options).
@@ -1393,17 +1404,21 @@ void launch_trace_nf(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs&
   const size_t smem = (size_t)kNfStack * kBlock * 4;
   const void* f = count ? (const void*)k_trace<true, false, ALPHA, false, kBlock, true>
                         : (const void*)k_trace<false, false, ALPHA, false, kBlock, true>;
-  // 80 VGPRs and kNfStack KiB of LDS per workgroup both allow 6 waves per
-  // SIMD: a full grid leaves the other queue's k_shade no VGPRs. The walk
-  // takes half (3 of 6 WG/CU): its vector-memory unit is the shared limit, so
-  // more of its waves buy nothing while k_shade beside it gains (profiles/
-  // r4_nf/tune.txt §6: 4 -> 3 WG/CU +0.8%, 2 WG/CU -14%)
-  const uint32_t grid = persistent_grid(c, f, smem, c->n_queues > 1, kBlock, 1, 2);
+  // kNfStack KiB of LDS per workgroup allow 6 waves per SIMD, its registers
+  // (<= 128 VGPRs: the rounding margins' state and code, round 5, would
+  // spill at 80) at least 4. Beside another queue the walk takes 3 WG/CU: its
+  // vector-memory unit is the shared limit, so more of its waves buy nothing
+  // while k_shade beside it gains (profiles/r4_nf/tune.txt §6: 4 -> 3 WG/CU
+  // +0.8%, 2 WG/CU -14%)
+  const uint32_t grid = persistent_grid(c, f, smem, c->n_queues > 1, kBlock, 1, 1);
+  const uint32_t nf_cap = 3u * (uint32_t)c->cus;
+  if (c->n_queues > 1 && !c->wgs_per_cu && grid > nf_cap) c->grids[std::make_pair(f, smem)] = nf_cap;
+  const uint32_t g = c->grids[std::make_pair(f, smem)];
   if (count)
-    hipLaunchKernelGGL((k_trace<true, false, ALPHA, false, kBlock, true>), dim3(grid), dim3(kBlock), smem, st, c->S, in,
+    hipLaunchKernelGGL((k_trace<true, false, ALPHA, false, kBlock, true>), dim3(g), dim3(kBlock), smem, st, c->S, in,
                        q.hits, q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
   else
-    hipLaunchKernelGGL((k_trace<false, false, ALPHA, false, kBlock, true>), dim3(grid), dim3(kBlock), smem, st, c->S, in,
+    hipLaunchKernelGGL((k_trace<false, false, ALPHA, false, kBlock, true>), dim3(g), dim3(kBlock), smem, st, c->S, in,
                        q.hits, q.ctrl, cur, c->d_cnt, tmin, tmax, c->tune);
 }
 
@@ -2132,6 +2147,7 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     S.vnf_leaf = (const uint32_t*)(base + o_vnf);
     for (int k = 0; k < 4; ++k) S.vnf_base[k] = hs.vnf_base[k];
     S.n_vnf = (uint32_t)(hs.vnf_leaf.size() / 2);
+    S.nfb = hs.nfb;
     c->S = S;
     c->scene_bytes = off;
     c->trace_lds = S.n_tlet > 0;
@@ -2143,6 +2159,7 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     c->scene_rng = hs.trav_rng;
     c->scene_ext = !hs.surf_ops.empty() || hs.bg_kind == MRT_BG_CUBEMAP;
     c->scene_nf = hs.nf_ok;
+    c->scene_nf_gen = hs.nf_ok && (hs.nfb.kw1 > 0.0f || hs.nfb.ko1 > 0.0f);
     c->nf_note = hs.nf_ok ? "" : hs.nf_note;
     apply_options(c);  // the per-scene rules of the options left at -1
     c->has_scene = true;

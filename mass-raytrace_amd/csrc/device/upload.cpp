@@ -434,7 +434,9 @@ void put_m4_12(std::vector<float>& dst, const float* m16) {
 }  // namespace
 
 bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err, bool sibling_layout) {
+  const bool keep = s.keep_nf_boxes;
   s = HostScene{};
+  s.keep_nf_boxes = keep;
   SurfResolver surf{d, s, err, {}, {}};
   Emitter e{d, s, err, {}, &surf};
   // materials

@@ -55,6 +55,13 @@ struct HostScene {
   std::vector<uint32_t> vnf_leaf;  // {parent, key} pairs
   uint32_t vnf_base[4] = {0, 0, 0, 0};
   std::string nf_note;  // why a scene has no NF trees
+  NfBound nfb{};         // the walk's rounding margins (nf_bound.h, nf_tree.cpp)
+  uint32_t nf_wild = 0;  // instances the world margin does not cover: never culled
+  // tools/slab_check: set before building to keep every leaf object's NF box
+  // (6 floats per vnf_leaf slot: mn xyz, mx xyz) and which instances are wild
+  bool keep_nf_boxes = false;
+  std::vector<float> nf_leaf_box;
+  std::vector<uint8_t> nf_inst_wild;
 };
 
 // Builds the verified near-first trees of a linearised scene (after

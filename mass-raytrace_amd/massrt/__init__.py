@@ -158,7 +158,7 @@ class MrtTuning(C.Structure):
 
 
 GATHER_AUTO, GATHER_PEER, GATHER_RCCL = 0, 1, 2
-TRAVERSAL_REFERENCE, TRAVERSAL_NEAR_FIRST = 0, 1
+TRAVERSAL_AUTO, TRAVERSAL_REFERENCE, TRAVERSAL_NEAR_FIRST = -1, 0, 1
 
 
 def parse_options(text: str, what: str = "options") -> dict:

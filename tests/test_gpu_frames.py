@@ -191,8 +191,12 @@ def test_options_and_tuning(scene, golden_dir):
     assert c.get_option("queues") == 2 and c.get_option("trace_box_min") == -1
     c.upload(scene)
     t = c.tuning()
-    assert t["queues"] == 2 and t["trace_box_min"] == 24 and t["trace_chunk"] == 512 and t["shade_waves"] == 8
-    assert c.get_option("traversal") == massrt.TRAVERSAL_REFERENCE and t["traversal"] == massrt.TRAVERSAL_REFERENCE
+    # traversal AUTO: sphere_grid takes the near-first walk (its own rules: refill 40, k_shade at 7)
+    assert c.get_option("traversal") == massrt.TRAVERSAL_AUTO and t["traversal"] == massrt.TRAVERSAL_NEAR_FIRST
+    assert t["queues"] == 2 and t["trace_box_min"] == 24 and t["trace_chunk"] == 512 and t["shade_waves"] == 7
+    c.set_option("traversal", massrt.TRAVERSAL_REFERENCE)
+    t = c.tuning()
+    assert t["traversal"] == massrt.TRAVERSAL_REFERENCE and t["trace_refill"] == 32 and t["shade_waves"] == 8
     c.set_option("traversal", massrt.TRAVERSAL_NEAR_FIRST)  # its own rules: refill 40, k_shade at 7
     t = c.tuning()
     assert t["traversal"] == massrt.TRAVERSAL_NEAR_FIRST and t["trace_refill"] == 40 and t["shade_waves"] == 7

