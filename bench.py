@@ -79,11 +79,23 @@ CACHE_PEAK_GBS = 36900.0
 TRACE_BYTES = {"node_visits": 32, "triangle_tests": 36, "sphere_tests": 16, "instance_entries": 48}
 TRACE_RAY_BYTES = 32 + 16  # ray origin+direction read, hit record written
 
-# k_shade's algorithmic bytes per shaded path: the path state
-# read (ro, rd, thr, rng: 4 x 16 B) + its hit record (16 B) and the state
-# written to the next pool (4 x 16 B); rad moves only for the rare path that
-# holds radiance (a Mix that emits and scatters), so it is not counted
-SHADE_BYTES = 4 * 16 + 16 + 4 * 16
+# k_shade's algorithmic bytes, from the counting
+# step's events: every shaded path reads its state (ro, rd, thr, rng: 4 x 16 B)
+# and hit record (16 B); a survivor writes its state to the next pool (4 x 16
+# B), a finished sample its 16-B result; every closest hit reads the shading
+# data of its primitive (§8d: 36 B normals + 24 B uv + 32 B material) and
+# every texel tap (counted per texel) 4 B of RGBA8. rad moves only for the
+# rare path that holds radiance (a Mix that emits and scatters): not counted.
+SHADE_READ_PATH, SHADE_WRITE_SURVIVOR, SHADE_WRITE_RESULT = 4 * 16 + 16, 4 * 16, 16
+SHADE_HIT, SHADE_TEXEL = 36 + 24 + 32, 4
+
+
+def shade_bytes(cnt) -> dict:
+    """k_shade's algorithmic read and write bytes over the counted step."""
+    shaded, finished = cnt.get("shaded", 0), min(cnt.get("samples", 0), cnt.get("shaded", 0))
+    reads = SHADE_READ_PATH * shaded + SHADE_HIT * cnt.get("closest_hits", 0) + SHADE_TEXEL * cnt.get("texel_taps", 0)
+    writes = SHADE_WRITE_SURVIVOR * (shaded - finished) + SHADE_WRITE_RESULT * finished
+    return {"reads": reads, "writes": writes, "total": reads + writes}
 
 
 def parse():
@@ -534,8 +546,16 @@ def roofline_for(a, scene, cnt, ks, samples_total, elapsed, n_gpus, plan, trav: 
     pmc_path = (Path(a.pmc_json) if (a.pmc_json and scene == a.scene and not trav)
                 else REPO / "profiles" / f"pmc_{scene}{tag}.json")
     pj = load_pmc(pmc_path, stamp)
+    pmc_basis = "this configuration"
+    if pj is None and n_gpus > 1:
+        # N > 1: each device runs the 1-GPU kernels on its shard of the tiles,
+        # so the N=1 profile of the same source, scene and frame stands for the
+        # per-device limiter (labelled; traffic per launch is not rescaled)
+        pj = load_pmc(pmc_path, {**stamp, "n_gpus": 1})
+        if pj is not None:
+            pmc_basis = "the N=1 profile of the same source and config, as each device's limiter (not re-measured at N)"
     lim = limiter(pj) if pj else {}
-    traffic = pj["kernels"]["k_trace"].get("hbm_bytes_per_launch") if pj else None
+    traffic = pj["kernels"]["k_trace"].get("hbm_bytes_per_launch") if (pj and pmc_basis == "this configuration") else None
     bound = "unmeasured (no PMC profile of this source and config)"
     if lim:  # the busiest unit; none at half its peak: the dependent record loads' latency binds
         cand = {"l1/ta": lim.get("ta_busy", 0.0), "hbm": lim.get("hbm", 0.0), "valu": lim.get("valu_busy", 0.0)}
@@ -550,6 +570,7 @@ def roofline_for(a, scene, cnt, ks, samples_total, elapsed, n_gpus, plan, trav: 
                  "frac": round(lim["hbm"], 4)} if "hbm" in lim else None),
         "limiter": {k: round(v, 4) for k, v in lim.items()} or None,
         "pmc": str(pmc_path.relative_to(REPO)) + f" (src {stamp['src']})" if pj else None,
+        "pmc_basis": pmc_basis if pj else None,
         "kernel": "k_trace + drain k_render<adopt>", "bytes_per_launch": round(bytes_per_launch),
         "avg_launch_ms": round(avg_ms, 4), "launches": int(trav_launches),
         "k_trace": {"launches": int(ks["trace_launches"]),
@@ -566,14 +587,17 @@ def roofline_for(a, scene, cnt, ks, samples_total, elapsed, n_gpus, plan, trav: 
     }
     shade = None
     if cnt.get("shaded") and ks["shade_launches"] > 0:
-        # k_shade: HBM-streaming (path state in and out), SHADE_BYTES per shaded path
-        shaded = cnt["shaded"] / max(cnt["samples"], 1) * samples_total
-        sb = SHADE_BYTES * shaded / ks["shade_launches"]
+        # k_shade: HBM-streaming (path state in and out, shading data, texels): shade_bytes()
+        sbc = shade_bytes(cnt)
+        scale = samples_total / max(cnt["samples"], 1) / ks["shade_launches"]  # counted step -> one timed launch
+        sb = sbc["total"] * scale
         sms = ks["shade_ms"] / ks["shade_launches"]
         shade = {"kernel": "k_shade", "bound": "hbm", "bytes_per_launch": round(sb), "avg_launch_ms": round(sms, 4),
                  "launches": int(ks["shade_launches"]), "achieved": round(sb / (sms * 1e-3) / 1e9, 1),
                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(sb / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                 "bytes_per_path": SHADE_BYTES, "paths_per_sample": round(cnt["shaded"] / max(cnt["samples"], 1), 4)}
+                 "reads_per_launch": round(sbc["reads"] * scale), "writes_per_launch": round(sbc["writes"] * scale),
+                 "bytes_per_path": round(sbc["total"] / max(cnt["shaded"], 1), 1),
+                 "paths_per_sample": round(cnt["shaded"] / max(cnt["samples"], 1), 4)}
         # the same kernel with ONE queue (option queues=1 profile, tools/profile.sh TAG=_solo): alone on the
         # GPU; in the bench run it shares the CUs with the other queue's k_trace by design
         pjs = load_pmc(REPO / "profiles" / f"pmc_{scene}_solo.json", stamp)
@@ -587,6 +611,10 @@ def roofline_for(a, scene, cnt, ks, samples_total, elapsed, n_gpus, plan, trav: 
         ksh = pj["kernels"].get("k_shade", {}) if pj else {}
         if ksh.get("hbm_bytes_per_launch"):  # PMC of the same source and config (rocprof's per-launch average)
             shade["traffic"] = round(ksh["hbm_bytes_per_launch"])
+            shade["traffic_over_algorithmic"] = round(ksh["hbm_bytes_per_launch"] / max(sb, 1), 3)
+            if ksh.get("FETCH_SIZE") is not None and ksh.get("WRITE_SIZE") is not None:
+                shade["traffic_reads"] = round(2 * ksh["FETCH_SIZE"] * 1024)  # x2: gfx950 FETCH_SIZE (pmc_summary.py)
+                shade["traffic_writes"] = round(ksh["WRITE_SIZE"] * 1024)
             shade["pmc_avg_launch_ms"] = round(ksh["avg_ns"] * 1e-6, 4)
             shade["limiter"] = {k: round(v, 4) for k, v in limiter(pj, "k_shade").items()}
     # north_star asks >= 40% of HBM peak during BVH traversal: the co-run and

@@ -427,6 +427,12 @@ int mrt_context_devices(mrt_ctx* ctx, int* n_devices, int* devices);
 /* the gather transport: "none" (one device), "peer", "rccl", or
  * "peer (...)" with the reason RCCL was not used */
 const char* mrt_context_transport(const mrt_ctx* ctx);
+/* Test hooks of the transport choice (no GPU needed): the library RCCL is
+ * opened from (NULL or "": librccl.so.1), and the transport
+ * mrt_create_multi would pick for these devices — opening RCCL but creating
+ * no communicators — written to buf (e.g. "peer (RCCL unavailable: ...)"). */
+int mrt_debug_rccl_library(const char* name);
+int mrt_debug_transport(int n_devices, const int* devices, char* buf, uint32_t len);
 
 /* ---- device-resident Image (main.rs:598-638, ABI v7) --------------------
  * The reference's Image {pass count, per-pixel (colour sum, depth sum),

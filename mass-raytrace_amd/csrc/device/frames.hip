@@ -19,12 +19,14 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <chrono>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -63,13 +65,19 @@ struct Rccl {
   const char* (*error_string)(ncclResult_t) = nullptr;
 };
 
+// the library RCCL is opened from (mrt_debug_rccl_library: a test points it
+// at a missing file to take the peer-copy fallback on a machine that has RCCL)
+std::string g_rccl_name = "librccl.so.1";
+bool g_rccl_tried = false;
+std::mutex g_rccl_mu;
 const Rccl& rccl() {
   static Rccl r;
-  static bool tried = false;
-  if (!tried) {
-    tried = true;
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  std::lock_guard<std::mutex> lk(g_rccl_mu);
+  if (!g_rccl_tried) {
+    g_rccl_tried = true;
+    r = Rccl{};
+    void* h = dlopen(g_rccl_name.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (!h && g_rccl_name == "librccl.so.1") h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
     if (h) {
       r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
       r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
@@ -81,7 +89,7 @@ const Rccl& rccl() {
     }
   }
   if (!r.comm_init_all || !r.group_start || !r.group_end || !r.send || !r.recv || !r.error_string)
-    throw Fail{MRT_ERR_HIP, "RCCL (librccl.so.1) is not available"};
+    throw Fail{MRT_ERR_HIP, "RCCL (" + g_rccl_name + ") is not available"};
   return r;
 }
 
@@ -263,6 +271,24 @@ void Frame::gather() {
   HIPF(hipStreamSynchronize(d[0].st));
   gather_bytes += bytes;
   gather_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// The gather transport of n devices (distinct: no repeats): "none" for one,
+// "peer" for repeated devices (a rehearsal on one GPU), else RCCL if
+// init_rccl() (open RCCL, create the communicators) succeeds, and peer copies
+// with the reason otherwise. mrt_create_multi and mrt_debug_transport share it.
+template <typename Init>
+std::string choose_transport(int n, bool distinct, Init&& init_rccl, bool& use_rccl) {
+  use_rccl = false;
+  if (n == 1) return "none";
+  if (!distinct) return "peer";
+  try {
+    init_rccl();
+    use_rccl = true;
+    return "rccl";
+  } catch (const Fail& e) {
+    return "peer (RCCL unavailable: " + e.msg + ")";
+  }
 }
 
 std::vector<mrt_ctx*> devices_of(mrt_ctx* ctx) {
@@ -448,24 +474,34 @@ int mrt_create_multi(int n, const int* devices, mrt_ctx** out) {
     hipDeviceEnablePeerAccess(devices[0], 0);
   }
   (void)hipGetLastError();
-  if (n == 1) {
-    m->transport = "none";
-  } else if (!m->distinct) {
-    m->transport = "peer";  // repeated devices (a rehearsal on one GPU)
-  } else {
-    // RCCL between distinct devices: opened and its communicators created
-    // now, so a missing or failing RCCL shows here and not after a render;
-    // the context then gathers with peer copies and says why
-    try {
-      ensure_comms(m);
-      m->rccl = true;
-      m->transport = "rccl";
-    } catch (const Fail& e) {
-      m->comms.clear();
-      m->transport = "peer (RCCL unavailable: " + e.msg + ")";
-    }
-  }
+  // RCCL between distinct devices: opened and its communicators created
+  // now, so a missing or failing RCCL shows here and not after a render;
+  // the context then gathers with peer copies and says why
+  m->transport = choose_transport(n, m->distinct, [&] { ensure_comms(m); }, m->rccl);
+  if (!m->rccl) m->comms.clear();
   *out = ctx_wrap_multi(m);
+  return MRT_OK;
+}
+
+int mrt_debug_rccl_library(const char* name) {
+  std::lock_guard<std::mutex> lk(g_rccl_mu);
+  g_rccl_name = name && *name ? name : "librccl.so.1";
+  g_rccl_tried = false;
+  return MRT_OK;
+}
+
+int mrt_debug_transport(int n, const int* devices, char* buf, uint32_t len) {
+  if (n < 1 || !devices || !buf || !len) {
+    ctx_set_error(nullptr, "mrt_debug_transport: need n >= 1 devices and a buffer");
+    return MRT_ERR_INVALID;
+  }
+  std::vector<int> sorted(devices, devices + n);
+  std::sort(sorted.begin(), sorted.end());
+  const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+  bool use = false;
+  // the loader only (no communicators: this runs without GPUs)
+  const std::string t = choose_transport(n, distinct, [] { rccl(); }, use);
+  snprintf(buf, len, "%s", t.c_str());
   return MRT_OK;
 }
 

@@ -535,7 +535,9 @@ __global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, RenderParams 
         rad = make_float4(L.x, L.y, L.z, 0.0f);
         rs = make_uint4((uint32_t)rng.s0, (uint32_t)(rng.s0 >> 32), (uint32_t)rng.s1, (uint32_t)(rng.s1 >> 32));
       } else {
+#ifndef MRT_PROBE_NO_RESULTS  // probe build (tools/shade_probe.sh): k_shade's HBM writes without the scattered results stores
         results[MRT_IDX(S, g, rp.G, 21)] = make_float4(L.x, L.y, L.z, __uint_as_float(k));
+#endif
         nsample += 1;
       }
     }

@@ -215,6 +215,7 @@ EXPORTED_SYMBOLS = [
     "mrt_create_multi", "mrt_context_devices", "mrt_image_create", "mrt_image_destroy", "mrt_image_clear",
     "mrt_image_render", "mrt_image_prepass", "mrt_image_read", "mrt_image_tonemap", "mrt_image_gather_stats",
     "mrt_build_info", "mrt_set_option", "mrt_get_option", "mrt_get_tuning", "mrt_context_transport", "mrt_image_gather",
+    "mrt_debug_rccl_library", "mrt_debug_transport",
 ]
 
 _lib = None
@@ -304,6 +305,8 @@ def lib() -> C.CDLL:
         "mrt_get_option": (I, [P, C.c_char_p, C.POINTER(I64)]),
         "mrt_get_tuning": (I, [P, C.POINTER(MrtTuning)]),
         "mrt_context_transport": (C.c_char_p, [P]),
+        "mrt_debug_rccl_library": (C.c_int, [C.c_char_p]),
+        "mrt_debug_transport": (C.c_int, [C.c_int, C.POINTER(C.c_int), C.c_char_p, C.c_uint32]),
         "mrt_image_gather": (I, [P]),
     }
     for name, (res, args) in sig.items():
@@ -498,6 +501,23 @@ def preorder(desc: MrtSceneDesc):
     for r in range(desc.n_roots):
         walk(desc.roots[r])
     return out, boxes
+
+
+def debug_transport(devices, rccl_library: str | None = None) -> str:
+    """The gather transport mrt_create_multi would pick for `devices`
+    (mrt_debug_transport; opens RCCL from `rccl_library`, default
+    librccl.so.1, creates no communicators: no GPU needed)."""
+    L = lib()
+    L.mrt_debug_rccl_library((rccl_library or "").encode())
+    try:
+        ids = (C.c_int * len(devices))(*devices)
+        buf = C.create_string_buffer(512)
+        rc = L.mrt_debug_transport(len(devices), ids, buf, 512)
+        if rc != 0:
+            raise MassrtError(f"mrt_debug_transport failed ({rc}): {L.mrt_global_last_error().decode()}")
+        return buf.value.decode()
+    finally:
+        L.mrt_debug_rccl_library(b"")
 
 
 def build_info() -> str:

@@ -93,3 +93,20 @@ def test_builder_errors_are_reported():
         b.build_bvh()  # BvhNode::new(vec![]) would recurse forever in the reference
     with pytest.raises(massrt.MassrtError, match="out of range"):
         b.material(massrt.MAT_LAMBERTIAN, surface=7)
+
+
+def test_transport_choice_and_rccl_fallback():
+    """mrt_create_multi's transport choice (frames.hip choose_transport),
+    without GPUs: one device "none", repeated devices "peer", distinct devices
+    RCCL when librccl opens, and — RCCL pointed at a missing library — the
+    peer-copy fallback with the reason in the transport text (VERDICT r4 #6)."""
+    import massrt
+
+    assert massrt.debug_transport([0]) == "none"
+    assert massrt.debug_transport([0, 0, 0]) == "peer"
+    t = massrt.debug_transport([0, 1], rccl_library="librccl_missing_for_test.so")
+    assert t.startswith("peer (RCCL unavailable: RCCL (librccl_missing_for_test.so) is not available"), t
+    # the real loader (ROCm's librccl is in this image): RCCL between distinct devices
+    assert massrt.debug_transport([0, 1, 2, 3, 4, 5, 6, 7]) == "rccl"
+    # the hook is reset: the next context opens the default library again
+    assert massrt.debug_transport([3, 5]) == "rccl"
