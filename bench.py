@@ -426,10 +426,15 @@ class MultiRunner:
 
     def reset_gather_stats(self):
         self.gathers = self.img.gather_stats()
+        self.dev_ms = self.img.device_stats()
 
     def gather_stats(self):
         b, ms = self.img.gather_stats()
         return b - self.gathers[0], ms - self.gathers[1]
+
+    def device_ms(self):
+        """Per-device render ms since reset_gather_stats (HIP events)."""
+        return [x - y for x, y in zip(self.img.device_stats(), self.dev_ms)]
 
     def mean_bounces(self):
         _, b, passes = self.img.read()
@@ -682,6 +687,7 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
                              "devices": devices, "transport": r.ctx.transport(),
                              "bytes_to_device0_per_step": round(g_bytes / steps),
                              "ms_per_step": round(g_ms / steps, 3),
+                             "device_render_ms_per_step": [round(x / steps, 3) for x in r.device_ms()],
                              "per_rank_ms_per_step": [round(e / steps * 1e3, 3) for e in per_rank]}
         else:
             out["gather"] = {"path": "one process per GPU: mrt_render_device + torch.distributed gather",

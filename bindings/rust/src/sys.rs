@@ -358,6 +358,8 @@ extern "C" {
     pub fn mrt_create_multi(n_devices: i32, devices: *const i32, out: *mut *mut mrt_ctx) -> i32;
     pub fn mrt_context_devices(ctx: *mut mrt_ctx, n_devices: *mut i32, devices: *mut i32) -> i32;
     pub fn mrt_context_transport(ctx: *const mrt_ctx) -> *const c_char;
+    pub fn mrt_debug_rccl_library(name: *const c_char) -> i32;
+    pub fn mrt_debug_transport(n_devices: i32, devices: *const i32, buf: *mut c_char, len: u32) -> i32;
 
     // ---- device-resident Image (main.rs:598-638, ABI v7)
     pub fn mrt_image_create(ctx: *mut mrt_ctx, width: u32, height: u32, out: *mut *mut mrt_image) -> i32;
@@ -370,6 +372,7 @@ extern "C" {
     pub fn mrt_image_gather(img: *mut mrt_image) -> i32;
     pub fn mrt_image_tonemap(img: *mut mrt_image, mode: u32, rgb8: *mut u8) -> i32;
     pub fn mrt_image_gather_stats(img: *mut mrt_image, bytes: *mut u64, ms: *mut f64) -> i32;
+    pub fn mrt_image_device_stats(img: *mut mrt_image, n_devices: i32, render_ms: *mut f64) -> i32;
 
     // ---- build identity (ABI v7)
     pub fn mrt_build_info() -> *const c_char;

@@ -469,6 +469,14 @@ int mrt_image_gather(mrt_image* img);
 int mrt_image_tonemap(mrt_image* img, uint32_t mode, uint8_t* rgb8);
 /* bytes that crossed between devices in the image's gathers, and their time */
 int mrt_image_gather_stats(mrt_image* img, uint64_t* bytes, double* ms);
+/* per-device render time so far (ms, HIP events around each device's share
+ * of every mrt_image_render; waits for renders still running); render_ms has
+ * one entry per device of the context */
+int mrt_image_device_stats(mrt_image* img, int n_devices, double* render_ms);
+/* per-device render time so far (ms, HIP events around each device's share
+ * of every mrt_image_render; waits for renders still running); render_ms has
+ * one entry per device of the context (ABI v8 addition) */
+int mrt_image_device_stats(mrt_image* img, int n_devices, double* render_ms);
 
 /* ---- build identity (ABI v7) -------------------------------------------
  * hash of the sources the library was built from (csrc/ + include/, as

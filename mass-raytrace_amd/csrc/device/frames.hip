@@ -115,6 +115,10 @@ struct DevFrame {
   uint32_t count = 0;  // pixels of this device's shard
   std::vector<uint32_t> pix;  // their indices, in slab order (host; mrt_render's per-shard upload)
   void* recv = nullptr;  // on device 0
+  // timing events around this device's renders not yet added to render_ms
+  // (mrt_image_device_stats collects them; a render never waits for them)
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  double render_ms = 0;  // this device's render time so far (HIP events)
 };
 
 // A frame over the devices of a context: device i owns shard si + i*sc of sc*n.
@@ -172,6 +176,7 @@ struct Frame {
       hipSetDevice(f.device);
       hipFree(f.rgb), hipFree(f.b), hipFree(f.slab);
       if (f.ev) hipEventDestroy(f.ev);
+      for (auto& e : f.pending) hipEventDestroy(e.first), hipEventDestroy(e.second);
       if (f.st) hipStreamDestroy(f.st);
     }
     if (!d.empty()) {
@@ -183,12 +188,25 @@ struct Frame {
 
   ~Frame() { release(); }
 
-  // every device renders its shard of `a` (a.shard_* ignored), concurrently
+  // every device renders its shard of `a` (a.shard_* ignored), concurrently;
+  // events around each device's render time it (collect_times)
   void render(const mrt_render_args& a0) {
+    auto one = [&](size_t i, mrt_render_args a) {
+      DevFrame& f = d[i];
+      HIPF(hipSetDevice(f.device));
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      HIPF(hipEventCreate(&e0));
+      HIPF(hipEventCreate(&e1));
+      f.pending.push_back({e0, e1});
+      HIPF(hipEventRecord(e0, f.st));
+      MRTF(f.ctx, mrt_render_device(f.ctx, &a, f.rgb, f.b, f.st));
+      HIPF(hipSetDevice(f.device));
+      HIPF(hipEventRecord(e1, f.st));
+    };
     if (d.size() == 1) {
       mrt_render_args a = a0;
       a.shard_index = si, a.shard_count = sc;
-      MRTF(d[0].ctx, mrt_render_device(d[0].ctx, &a, d[0].rgb, d[0].b, d[0].st));
+      one(0, a);
       return;
     }
     std::vector<Fail> fails(d.size(), Fail{MRT_OK, ""});
@@ -197,8 +215,11 @@ struct Frame {
       th.emplace_back([&, i] {
         mrt_render_args a = a0;
         a.shard_index = shard(i), a.shard_count = shards();
-        const int rc = mrt_render_device(d[i].ctx, &a, d[i].rgb, d[i].b, d[i].st);
-        if (rc != MRT_OK) fails[i] = Fail{rc, mrt_last_error(d[i].ctx)};
+        try {
+          one(i, a);
+        } catch (const Fail& e) {
+          fails[i] = e;
+        }
       });
     for (auto& t : th) t.join();
     for (const Fail& f : fails)
@@ -207,6 +228,22 @@ struct Frame {
 
   // the other devices' tiles onto device 0's buffers (pack, send, unpack)
   void gather();
+
+  // adds every finished render's event time to its device's render_ms
+  // (waits for renders still running)
+  void collect_times() {
+    for (DevFrame& f : d) {
+      HIPF(hipSetDevice(f.device));
+      for (auto& e : f.pending) {
+        HIPF(hipEventSynchronize(e.second));
+        float ms = 0;
+        HIPF(hipEventElapsedTime(&ms, e.first, e.second));
+        f.render_ms += ms;
+        hipEventDestroy(e.first), hipEventDestroy(e.second);
+      }
+      f.pending.clear();
+    }
+  }
 };
 
 }  // namespace
@@ -660,6 +697,15 @@ int mrt_image_gather_stats(mrt_image* img, uint64_t* bytes, double* ms) {
   if (bytes) *bytes = img->f.gather_bytes;
   if (ms) *ms = img->f.gather_ms;
   return MRT_OK;
+}
+
+int mrt_image_device_stats(mrt_image* img, int n, double* render_ms) {
+  if (!img) return MRT_ERR_INVALID;
+  return guard(img->ctx, [&] {
+    if (!render_ms || n < (int)img->f.d.size()) throw Fail{MRT_ERR_INVALID, "render_ms needs one entry per device"};
+    img->f.collect_times();
+    for (size_t i = 0; i < img->f.d.size(); ++i) render_ms[i] = img->f.d[i].render_ms;
+  });
 }
 
 }  // extern "C"

@@ -215,7 +215,7 @@ EXPORTED_SYMBOLS = [
     "mrt_create_multi", "mrt_context_devices", "mrt_image_create", "mrt_image_destroy", "mrt_image_clear",
     "mrt_image_render", "mrt_image_prepass", "mrt_image_read", "mrt_image_tonemap", "mrt_image_gather_stats",
     "mrt_build_info", "mrt_set_option", "mrt_get_option", "mrt_get_tuning", "mrt_context_transport", "mrt_image_gather",
-    "mrt_debug_rccl_library", "mrt_debug_transport",
+    "mrt_debug_rccl_library", "mrt_debug_transport", "mrt_image_device_stats",
 ]
 
 _lib = None
@@ -306,6 +306,7 @@ def lib() -> C.CDLL:
         "mrt_get_tuning": (I, [P, C.POINTER(MrtTuning)]),
         "mrt_context_transport": (C.c_char_p, [P]),
         "mrt_debug_rccl_library": (C.c_int, [C.c_char_p]),
+        "mrt_image_device_stats": (C.c_int, [P, C.c_int, C.POINTER(C.c_double)]),
         "mrt_debug_transport": (C.c_int, [C.c_int, C.POINTER(C.c_int), C.c_char_p, C.c_uint32]),
         "mrt_image_gather": (I, [P]),
     }
@@ -834,6 +835,13 @@ class Image:
         b, ms = C.c_uint64(), C.c_double()
         self._check(lib().mrt_image_gather_stats(self.h, C.byref(b), C.byref(ms)))
         return int(b.value), float(ms.value)
+
+    def device_stats(self) -> list:
+        """Per-device render ms so far (HIP events around each device's share of every render)."""
+        n = len(self.ctx.devices())
+        out = (C.c_double * n)()
+        self._check(lib().mrt_image_device_stats(self.h, n, out))
+        return [float(x) for x in out]
 
 
 # ---- render(): the drop-in pass loop (mirror of bindings/rust/src/lib.rs) ---

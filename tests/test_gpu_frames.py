@@ -124,6 +124,8 @@ def test_multi_device_image_gathers_each_tile_once(scene):
     sent, _ = img.gather_stats()
     n1, n2 = (massrt.shard_pixels(W, H, i, 3).size for i in (1, 2))
     assert sent == 16 * (n1 + n2)  # device 0's own tiles never move
+    ms = img.device_stats()  # every device rendered its share of both calls (HIP events)
+    assert len(ms) == 3 and all(x > 0 for x in ms), ms
     assert np.array_equal(img.tonemap(), one.tonemap(W, H, ref[0], ref[1], 4))
     img.close()
     multi.close()
