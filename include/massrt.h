@@ -339,7 +339,10 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  *   gather            MRT_GATHER_* (multi-device contexts)
  *   traversal         MRT_TRAVERSAL_* (default AUTO: per scene); NEAR_FIRST
  *                     applies to scenes without traversal draws (Volume, Mix
- *                     alpha) and without a treelet, others keep REFERENCE
+ *                     alpha) and without a treelet, others keep REFERENCE.
+ *                     The near-first trees are built at upload for the value
+ *                     then in effect (REFERENCE: none; AUTO: where it would
+ *                     walk near first): set NEAR_FIRST before uploading
  *   nf_kappa_log2     -40..-8  NEAR_FIRST: rays whose generic-triangle kappa
  *                     (nf_bound.h) exceeds 2^v take the reference walk (-8)
  *   trace_nf_batch    -1, 1..64  NEAR_FIRST: finished walks checked together

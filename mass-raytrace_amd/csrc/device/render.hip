@@ -2056,6 +2056,9 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     if (!d) throw ApiError{MRT_ERR_INVALID, "null scene"};
     HostScene hs;
     std::string err;
+    // NF trees per the option in effect at upload (upload.h nf_build)
+    hs.nf_build = c->opt[OPT_TRAVERSAL] == MRT_TRAVERSAL_REFERENCE ? kNfBuildNever
+                  : c->opt[OPT_TRAVERSAL] == MRT_TRAVERSAL_NEAR_FIRST ? kNfBuildAlways : kNfBuildAuto;
     if (!build_host_scene(*d, hs, err)) throw ApiError{MRT_ERR_INVALID, err};
     build_treelet(hs, (uint32_t)((size_t)c->treelet_kb * 1024 / 16));
     // one allocation, 256-B aligned sections

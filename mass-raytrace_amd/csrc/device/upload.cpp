@@ -435,8 +435,10 @@ void put_m4_12(std::vector<float>& dst, const float* m16) {
 
 bool build_host_scene(const mrt_scene_desc& d, HostScene& s, std::string& err, bool sibling_layout) {
   const bool keep = s.keep_nf_boxes;
+  const int nf_build = s.nf_build;
   s = HostScene{};
   s.keep_nf_boxes = keep;
+  s.nf_build = nf_build;
   SurfResolver surf{d, s, err, {}, {}};
   Emitter e{d, s, err, {}, &surf};
   // materials

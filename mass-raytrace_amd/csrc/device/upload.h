@@ -60,9 +60,16 @@ struct HostScene {
   // tools/slab_check: set before building to keep every leaf object's NF box
   // (6 floats per vnf_leaf slot: mn xyz, mx xyz) and which instances are wild
   bool keep_nf_boxes = false;
+  // which NF trees to build (set before build_host_scene; the option
+  // "traversal" at upload): kNfBuildAuto builds them unless the per-scene
+  // rule would walk the reference's way anyway (a generic-triangle term, or a
+  // big instanced world), kNfBuildNever skips them, kNfBuildAlways builds them
+  int nf_build = 2;
   std::vector<float> nf_leaf_box;
   std::vector<uint8_t> nf_inst_wild;
 };
+
+enum { kNfBuildNever = 0, kNfBuildAlways = 1, kNfBuildAuto = 2 };
 
 // Builds the verified near-first trees of a linearised scene (after
 // build_host_scene; layout.h). A scene whose traversal draws random numbers,

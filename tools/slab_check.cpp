@@ -489,6 +489,7 @@ int main(int argc, char** argv) {
   mrt_builder_desc(b, &d, &cam);
   HostScene s;
   s.keep_nf_boxes = true;  // the bound checks' leaf boxes
+  s.nf_build = kNfBuildAlways;  // the trees even where the per-scene rule would walk the reference's way
   std::string err;
   if (!build_host_scene(d, s, err)) {
     printf("%s\n", err.c_str());
