@@ -906,16 +906,10 @@ MRT_DEV void nf_node_test(const uint4& s0, const uint4& s1, const TRay& r, float
   if (tray_fast(r)) {
     const float ax = sc.x * r.yx, ay = sc.y * r.yy, az = sc.z * r.yz;
     const float bx = fmaf(o.x, r.yx, -r.oyx), by = fmaf(o.y, r.yy, -r.oyy), bz = fmaf(o.z, r.yz, -r.oyz);
-#ifdef MRT_NF_YMAX  // experiment: the thickening as one t margin rho * 2 max|y| per child
-    const float lbx = bx, lby = by, lbz = bz, hbx = bx, hby = by, hbz = bz;
-    const float mabs = fmaf(vmax3(fabsf(bx), fabsf(by), fabsf(bz)), 0x1p-20f, fabsf(r.om)) +
-                       nfm * (2.0f * vmax3(fabsf(r.yx), fabsf(r.yy), fabsf(r.yz)) * (1.0f + 0x1p-20f));
-#else
     const float lbx = fmaf(-nfm, r.yx, bx), lby = fmaf(-nfm, r.yy, by), lbz = fmaf(-nfm, r.yz, bz);
     const float hbx = fmaf(nfm, r.yx, bx), hby = fmaf(nfm, r.yy, by), hbz = fmaf(nfm, r.yz, bz);
     const float mabs = fmaf(vmax1(vmax3(fabsf(lbx), fabsf(lby), fabsf(lbz)), vmax3(fabsf(hbx), fabsf(hby), fabsf(hbz))),
                             0x1p-20f, fabsf(r.om));
-#endif
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int b = 6 * c;
