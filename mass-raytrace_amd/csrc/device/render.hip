@@ -1225,7 +1225,9 @@ void set_device(mrt_ctx* c) { HIP_CHECK(hipSetDevice(c->device)); }
 // Derived fields from the options; options left at -1 take the per-scene
 // rules (scene_big / scene_instances, set at upload):
 //  * box run / refill (profiles/r2_tune, r3_tune.txt): refill 32
-//    everywhere; box run while >= 16 lanes are at a box for an
+//    except 12 for a big instanced world (Menger 50.0 -> 53.0 at 64 spp per
+//    step, 57.4 -> 58.8 at 256 with 16; mesh_ply keeps 32: 1148.7 vs 1125.9
+//    at 24; profiles/r5_nf_probe/summary.txt); box run while >= 16 lanes are at a box for an
 //    instance-heavy world (cube_field 266 -> 275, Menger 37.3 -> 44.1
 //    Msamples/s), >= 32 for another stream past half the chip's L2 (its
 //    record round trips go to the Infinity Cache; mesh_ply 749 -> 775), else
@@ -1262,7 +1264,7 @@ void apply_options(mrt_ctx* c) {
   c->finish_paths = (uint32_t)o[OPT_FINISH_PATHS];
   c->finish_grid_div = (uint32_t)o[OPT_FINISH_GRID_DIV];
   c->tune.refill = o[OPT_TRACE_REFILL] >= 0 ? (uint32_t)std::max<int64_t>(1, o[OPT_TRACE_REFILL])
-                                            : ((nf && !big_solid) ? 40u : 32u);
+                                            : ((nf && !big_solid) ? 40u : (inst && big) ? 12u : 32u);
   c->tune.box_min = o[OPT_TRACE_BOX_MIN] >= 0 ? (uint32_t)std::max<int64_t>(1, o[OPT_TRACE_BOX_MIN])
                                               : (inst ? 16u : (big ? (nf ? 28u : 32u) : 24u));
   c->tune.chunk = o[OPT_TRACE_CHUNK] >= 0 ? (uint32_t)o[OPT_TRACE_CHUNK]

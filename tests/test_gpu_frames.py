@@ -209,6 +209,7 @@ def test_options_and_tuning(scene, golden_dir):
     c.set_option("trace_box_min", -1)
     c.upload(cube)  # > 1000 instances: box run from 16 lanes, grabs of 128
     assert c.tuning()["trace_box_min"] == 16 and c.tuning()["trace_chunk"] == 128
+    assert c.tuning()["trace_refill"] == 32  # 12 only for a big instanced world (Menger)
     for name, bad in (("queues", 5), ("trace_block", 300), ("shade_waves", 6), ("trace_chunk", 8), ("trace_nf_batch", 0),
                       ("traversal", 2)):
         with pytest.raises(massrt.MassrtError, match=name):
