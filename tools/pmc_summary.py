@@ -31,16 +31,17 @@ scene = sys.argv[2] if len(sys.argv) > 2 else "sphere_grid"
 
 
 def traced_config():
-    """(width, height, spp per step) of the bench line the trace run printed."""
+    """(width, height, spp per step, walk) of the bench line the trace run
+    printed (walk: the traversal the context took, MRT_TRAVERSAL_*)."""
     lines = (out_dir / "trace.log").read_text().splitlines() if (out_dir / "trace.log").exists() else []
     for ln in reversed(lines):
         if ln.startswith("{"):
             c = json.loads(ln)["config"]
-            return c["width"], c["height"], c["spp_per_step"]
-    raise SystemExit(f"no bench line in {out_dir / 'trace.log'}: pass W H SPP")
+            return c["width"], c["height"], c["spp_per_step"], int(c.get("tuning", {}).get("traversal", 0))
+    raise SystemExit(f"no bench line in {out_dir / 'trace.log'}: pass W H SPP TRAVERSAL")
 
 
-W, H, SPP = (int(x) for x in sys.argv[3:6]) if len(sys.argv) > 5 else traced_config()
+W, H, SPP, TRAV = (int(x) for x in sys.argv[3:7]) if len(sys.argv) > 6 else traced_config()
 N_CU, N_XCD = 256, 8
 
 
@@ -61,9 +62,8 @@ import bench  # noqa: E402  (source hash of the library the profile measured)
 
 summary = {"scene": scene, "width": W, "height": H,
            "stamp": {"scene": scene, "width": W, "height": H, "spp_per_step": SPP, "src": bench.src_hash(),
-                     # the walk profiled (MASSRT_OPTIONS traversal=1: the near-first walk, TAG=_nf)
-                     "traversal": int(dict(kv.split("=") for kv in os.environ.get("MASSRT_OPTIONS", "").split(",")
-                                           if "=" in kv).get("traversal", 0))},
+                     # the walk profiled, as the bench line reports it (AUTO resolved per scene)
+                     "traversal": TRAV},
            "kernels": {}}
 for r in rows("trace/**/*kernel_stats.csv"):
     name = short(r.get("Name", r.get("KernelName", "")))
@@ -118,7 +118,8 @@ if "hbm_bytes_per_launch" in t:
 print(json.dumps(summary, indent=1))
 
 
-tag = os.environ.get("PMC_TAG", "")
+# bench.py reads profiles/pmc_<scene>_nf.json for the near-first walk, pmc_<scene>_solo.json (PMC_TAG) alone
+tag = os.environ.get("PMC_TAG", "") or ("_nf" if TRAV == 1 else "")
 if tag:
     summary["tag"] = tag
     summary["options"] = os.environ.get("MASSRT_OPTIONS", "")
