@@ -44,8 +44,11 @@ roofline (dominant kernel k_trace, closest hit):
              hash) matches this run; else null.
   bound    = the unit the PMC counters show busiest (TA/L1 address path, HBM,
              VALU), e.g. "l1/ta" for SphereGrid.
-roofline_k_shade: k_shade (path-state streaming) against HBM, 144 B per
-  shaded path, with the PMC traffic/limiter of the same stamped profile.
+roofline_k_shade: k_shade (path-state streaming) against HBM: per shaded
+  path the state read and the survivor's state or the finished result
+  written, plus the shading data of each closest hit and the texels
+  (shade_bytes), with the PMC traffic/limiter of the same stamped profile
+  and the waves' material coherence (ABI v9 counters).
 cpu_baseline: the oracle's reference-mode restatement (main.rs:159-290
 threading: num_cpus-2 workers rendering whole 1-spp passes) on a stratified
 sample of rows spread over the whole frame, rank 0 at N=1 only, plus an
@@ -603,6 +606,12 @@ def roofline_for(a, scene, cnt, ks, samples_total, elapsed, n_gpus, plan, trav: 
                  "reads_per_launch": round(sbc["reads"] * scale), "writes_per_launch": round(sbc["writes"] * scale),
                  "bytes_per_path": round(sbc["total"] / max(cnt["shaded"], 1), 1),
                  "paths_per_sample": round(cnt["shaded"] / max(cnt["samples"], 1), 4)}
+        if cnt.get("shade_waves"):  # ABI v9: how material-coherent a shading wave is
+            shade["coherence"] = {"kinds_per_wave": round(cnt["shade_kinds"] / cnt["shade_waves"], 3),
+                                  "materials_per_wave": round(cnt["shade_materials"] / cnt["shade_waves"], 3),
+                                  "note": "distinct material kinds (a miss = one more) and material indices among "
+                                          "a k_shade wave's lanes, counting step; a material-sorted pool could bring "
+                                          "both to ~1"}
         # the same kernel with ONE queue (option queues=1 profile, tools/profile.sh TAG=_solo): alone on the
         # GPU; in the bench run it shares the CUs with the other queue's k_trace by design
         pjs = load_pmc(REPO / "profiles" / f"pmc_{scene}_solo.json", stamp)

@@ -1,4 +1,4 @@
-//! Raw FFI of include/massrt.h, MRT_ABI_VERSION 8.
+//! Raw FFI of include/massrt.h, MRT_ABI_VERSION 9.
 //!
 //! Every struct is `#[repr(C)]` with the header's field order and types;
 //! tests/test_rust_binding.py parses this file and checks each struct's
@@ -8,7 +8,7 @@
 
 use std::os::raw::{c_char, c_void};
 
-pub const MRT_ABI_VERSION: i32 = 8;
+pub const MRT_ABI_VERSION: i32 = 9;
 
 pub const MRT_OK: i32 = 0;
 pub const MRT_ERR_INVALID: i32 = 1;
@@ -263,6 +263,9 @@ pub struct mrt_counters {
     pub box_exact: u64,
     pub shaded: u64,
     pub vnf_fallbacks: u64,
+    pub shade_waves: u64,
+    pub shade_kinds: u64,
+    pub shade_materials: u64,
 }
 
 #[repr(C)]

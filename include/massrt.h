@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 8
+#define MRT_ABI_VERSION 9
 
 /* ---- status codes ------------------------------------------------------ */
 #define MRT_OK 0
@@ -262,6 +262,12 @@ typedef struct {
   /* near-first walks whose hit the reference's walk would not reach: walked
      again the reference's way (ABI v8) */
   uint64_t vnf_fallbacks;
+  /* shading coherence of the counting k_shade (ABI v9): waves with work, and
+     summed over them the distinct material kinds (a miss: one more) and the
+     distinct material indices among their lanes */
+  uint64_t shade_waves;
+  uint64_t shade_kinds;
+  uint64_t shade_materials;
 } mrt_counters;
 
 /* Kernel timing accumulated by renders flagged MRT_RENDER_TIME_KERNELS

@@ -27,12 +27,14 @@ MRT_DEV uint32_t make_ref(uint32_t kind, uint32_t idx) { return (kind << 28) | i
 
 struct DevCounters {
   unsigned long long samples, segments, node_visits, sphere_tests, triangle_tests, instance_entries,
-      model_entries, closest_hits, texel_taps, bounces, wave_slots, lane_steps, box_exact, shaded, vnf_fallbacks;
+      model_entries, closest_hits, texel_taps, bounces, wave_slots, lane_steps, box_exact, shaded, vnf_fallbacks,
+      shade_waves, shade_kinds, shade_materials;
 };
 
 struct LocalCounters {
   uint32_t node_visits = 0, sphere_tests = 0, triangle_tests = 0, instance_entries = 0, model_entries = 0,
-           texel_taps = 0, wave_slots = 0, lane_steps = 0, box_exact = 0, vnf_fallbacks = 0;
+           texel_taps = 0, wave_slots = 0, lane_steps = 0, box_exact = 0, vnf_fallbacks = 0, shade_waves = 0,
+           shade_kinds = 0, shade_materials = 0;
 };
 
 // Bounds checks of every scene-array index, compiled in with

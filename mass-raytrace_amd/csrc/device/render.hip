@@ -133,12 +133,12 @@ __device__ __forceinline__ uint32_t wg_reserve(uint32_t* counter, uint32_t count
 
 __device__ void flush_counters(DevCounters* c, const LocalCounters& lc, uint32_t segs, uint32_t hits,
                                uint32_t samples, uint32_t bounces, uint32_t shaded = 0) {
-  uint32_t v[15] = {samples, segs, lc.node_visits, lc.sphere_tests, lc.triangle_tests, lc.instance_entries,
-                    lc.model_entries, hits, lc.texel_taps, bounces, lc.wave_slots, lc.lane_steps, lc.box_exact, shaded,
-                    lc.vnf_fallbacks};
+  uint32_t v[18] = {samples,         segs,           lc.node_visits, lc.sphere_tests,   lc.triangle_tests, lc.instance_entries,
+                    lc.model_entries, hits,           lc.texel_taps,  bounces,           lc.wave_slots,     lc.lane_steps,
+                    lc.box_exact,     shaded,         lc.vnf_fallbacks, lc.shade_waves, lc.shade_kinds,    lc.shade_materials};
   unsigned long long* dst = reinterpret_cast<unsigned long long*>(c);
 #pragma unroll
-  for (int k = 0; k < 15; ++k) {
+  for (int k = 0; k < 18; ++k) {
     uint32_t s = wave_sum(v[k]);
     if (lane_id() == 0 && s) atomicAdd(dst + k, (unsigned long long)s);
   }
@@ -461,14 +461,19 @@ __global__ __launch_bounds__(kBlock) void k_trace_simple(DevScene S, PathBufs in
 // ray (o, d): adds T * emitted (hit) or T * background (miss) to L; on a
 // scatter that continues (and depth left) moves (o, d) to the scattered ray,
 // multiplies T by the attenuation and returns true.
+// (mat: the hit's material index, kShadeMiss for a miss: the counting
+// k_shade's coherence counters)
+constexpr uint32_t kShadeMiss = 0xFFFFFFFEu, kShadeIdle = 0xFFFFFFFFu;
 template <bool EXT>
 MRT_DEV bool shade_step(const DevScene& S, uint32_t max_depth, const Hit& h, V3& o, V3& d, V3& T, V3& L, uint32_t& k,
-                        PathRng& rng, LocalCounters& lc, uint32_t& nbounce) {
+                        PathRng& rng, LocalCounters& lc, uint32_t& nbounce, uint32_t& mat) {
   if (h.prim == kRefNone) {
+    mat = kShadeMiss;
     L = L + T * background<EXT>(S, d, lc);
     return false;
   }
   Surf s = resolve_hit(S, o, d, h);
+  mat = s.material;
   V3 emitted, atten, nd;
   bool cont = scatter<EXT>(S, s, d, rng, emitted, atten, nd, lc);
   L = L + T * emitted;
@@ -479,6 +484,30 @@ MRT_DEV bool shade_step(const DevScene& S, uint32_t max_depth, const Hit& h, V3&
   o = s.point;
   d = nd;
   return k < max_depth;  // trace(depth 0) returns (0, 0)
+}
+
+// How coherent a k_shade wave's shading is (counting launches only; SURVEY
+// §7 step 7 asks whether sorting rays by material would pay): per wave with
+// work, the distinct material kinds among its lanes (a miss counts as one
+// more kind: the background branch) — the branches the wave executes one
+// after another — and the distinct material indices (the material records
+// it gathers). A material-sorted pool could bring both to ~1.
+MRT_DEV void shade_coherence(const DevScene& S, uint32_t mat, LocalCounters& lc) {
+  const unsigned long long act = __ballot(mat != kShadeIdle);
+  if (act == 0) return;
+  const uint32_t kind = mat == kShadeIdle ? 0xFFu : mat == kShadeMiss ? 16u : S.materials[MRT_IDX(S, mat, S.n_materials, 4)].kind;
+  uint32_t nk = 0, nm = 0;
+  for (uint32_t kk = 0; kk <= 16; ++kk) nk += __ballot(kind == kk) != 0;
+  for (unsigned long long rem = act; rem;) {
+    const uint32_t m0 = __shfl(mat, __ffsll((long long)rem) - 1, 64);
+    rem &= ~__ballot(mat == m0);
+    ++nm;
+  }
+  if (lane_id() == 0) {
+    lc.shade_waves += 1;
+    lc.shade_kinds += nk;
+    lc.shade_materials += nm;
+  }
 }
 
 // k_shade only shades and compacts: new camera rays go in behind the
@@ -513,6 +542,7 @@ __global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, RenderParams 
     bool alive = false;
     float4 ro{}, rd{}, thr{}, rad{};
     uint4 rs{};
+    uint32_t mat = kShadeIdle;
     if (i < n) {
       nshaded += 1;
       ro = in.ro[i];
@@ -526,7 +556,7 @@ __global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, RenderParams 
       uint32_t g = __float_as_uint(ro.w), k = __float_as_uint(rd.w);
       PathRng rng{(unsigned long long)rs.x | ((unsigned long long)rs.y << 32),
                   (unsigned long long)rs.z | ((unsigned long long)rs.w << 32)};
-      const bool cont = shade_step<EXT>(S, rp.max_depth, h, o, d, T, L, k, rng, lc, nbounce);
+      const bool cont = shade_step<EXT>(S, rp.max_depth, h, o, d, T, L, k, rng, lc, nbounce, mat);
       if (cont) {
         alive = true;
         ro = make_float4(o.x, o.y, o.z, __uint_as_float(g));
@@ -541,6 +571,7 @@ __global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, RenderParams 
         nsample += 1;
       }
     }
+    if (COUNT) shade_coherence(S, mat, lc);
     // compact the survivors into the next pool: one atomic per workgroup
     // (same-address atomics from every wave serialise in L2)
     const unsigned long long alive_mask = __ballot(alive);
@@ -649,7 +680,8 @@ __global__ __launch_bounds__(kBlock) void k_render(DevScene S, DevCamera cam, Re
         nh += h.prim != kRefNone;
         const float4 o4 = slot_ro[slot], d4 = slot_rd[slot];
         V3 o{o4.x, o4.y, o4.z}, d{d4.x, d4.y, d4.z};
-        if (shade_step<false>(S, rp.max_depth, h, o, d, T, L, k, rng, lc, nbounces)) {
+        uint32_t mat;
+        if (shade_step<false>(S, rp.max_depth, h, o, d, T, L, k, rng, lc, nbounces, mat)) {
           slot_ro[slot] = make_float4(o.x, o.y, o.z, 0.0f);
           slot_rd[slot] = make_float4(d.x, d.y, d.z, 0.0f);
           trav_init(tin, t, slot, INFINITY);
@@ -2354,6 +2386,9 @@ int mrt_get_counters(mrt_ctx* c, mrt_counters* out) {
     out->box_exact = h.box_exact;
     out->shaded = h.shaded;
     out->vnf_fallbacks = h.vnf_fallbacks;
+    out->shade_waves = h.shade_waves;
+    out->shade_kinds = h.shade_kinds;
+    out->shade_materials = h.shade_materials;
   });
 }
 

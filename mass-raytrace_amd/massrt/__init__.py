@@ -27,7 +27,7 @@ LIB_PATH = (Path(_SEL) if _SEL.endswith(".so") else
 REPO = _HERE.parent.parent
 
 # ---- constants (massrt.h) --------------------------------------------------
-ABI_VERSION = 8  # MRT_ABI_VERSION this binding was written for
+ABI_VERSION = 9  # MRT_ABI_VERSION this binding was written for
 REF_NONE, REF_NODE, REF_SPHERE, REF_TRIANGLE, REF_INSTANCE, REF_MODEL, REF_VOLUME = range(7)
 MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_SPECULAR, MAT_ISOTROPHIC, MAT_MIX = range(8)
 WRAP_MIRROR, WRAP_REPEAT, WRAP_CLAMP = range(3)
@@ -185,7 +185,8 @@ def env_options(env=None) -> dict:
 
 
 # scheduling counters of the persistent k_trace (no reference counterpart)
-SCHED_FIELDS = ["wave_slots", "lane_steps", "box_exact", "shaded", "vnf_fallbacks"]
+SCHED_FIELDS = ["wave_slots", "lane_steps", "box_exact", "shaded", "vnf_fallbacks", "shade_waves", "shade_kinds",
+                "shade_materials"]
 
 
 class MrtCounters(C.Structure):

@@ -24,7 +24,7 @@ def test_header_symbols_exported():
 
 
 def test_abi_version():
-    assert massrt.lib().mrt_abi_version() == massrt.ABI_VERSION == 8
+    assert massrt.lib().mrt_abi_version() == massrt.ABI_VERSION == 9
 
 
 def test_struct_layouts_match_header(tmp_path):

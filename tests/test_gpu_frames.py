@@ -91,6 +91,25 @@ def test_multi_device_context_render_equals_one_device(scene):
     one.close()
 
 
+def test_shading_coherence_counters(scene, golden_dir):
+    """ABI v9: the counting k_shade reports, per wave with work, the distinct
+    material kinds (a miss counts as one more kind) and material indices of
+    its lanes. Bounds that hold for any pool order: at least one wave per 64
+    shaded paths, at most one per path; 1 <= kinds <= materials <= 64 per
+    wave. (finish_paths 0: no drain hand-off, k_shade shades every segment.)"""
+    for name, src, w, h in (("sphere_grid", scene, W, H), ("cornell", None, 48, 27)):
+        c = massrt.Context(0, options={"finish_paths": 0})
+        c.upload(src if src is not None else massrt.Builder(1).builtin(name, ASPECT, golden_dir))
+        c.reset_counters()
+        c.render(w, h, 0, 2, seed=5, counters=True)
+        k = c.counters()
+        waves, shaded = k["shade_waves"], k["shaded"]
+        assert shaded == k["segments"] > 0 and -(-shaded // 64) <= waves <= shaded, name
+        assert waves <= k["shade_kinds"] <= k["shade_materials"] <= 64 * waves, name
+        assert k["shade_kinds"] > waves, name  # several kinds share waves (lights, diffuse, glass, metal, sky)
+        c.close()
+
+
 @pytest.mark.parametrize("devices", [[0, 0, 0], [0]])
 def test_multi_device_shards_accumulate_into_one_host_buffer(scene, devices):
     """A caller that renders shard 0 then shard 1 of 2 into ONE nonzero host
