@@ -298,6 +298,7 @@ pub struct mrt_tuning {
     pub pool_paths: u64,
     pub results_max: u64,
     pub traversal: u32,
+    pub shade_bin: u32,
 }
 
 /// Context option "traversal" (ABI v8).

@@ -353,6 +353,10 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  *                     (nf_bound.h) exceeds 2^v take the reference walk (-8)
  *   trace_nf_batch    -1, 1..64  NEAR_FIRST: finished walks checked together
  *                     once this many lanes wait (-1: the refill threshold)
+ *   shade_bin         -1, 0, 1  k_shade writes each workgroup's surviving
+ *                     paths into the next pool grouped by the material kind
+ *                     they scattered from, so k_trace's waves walk rays of one
+ *                     kind together (-1: on); images are identical either way
  * Every render sizes its path pool and results slab to the device memory
  * free at that moment minus mem_reserve_mb (several contexts may share a
  * device), shrinking the pool first and then the samples per chunk. */
@@ -387,6 +391,7 @@ typedef struct {
   uint32_t queues, trace_refill, trace_box_min, trace_chunk, shade_waves;
   uint64_t pool_paths, results_max;
   uint32_t traversal; /* the walk k_trace uses for this scene (MRT_TRAVERSAL_*) */
+  uint32_t shade_bin; /* survivors grouped by material kind (option shade_bin; ABI v9) */
 } mrt_tuning;
 int mrt_get_tuning(mrt_ctx* ctx, mrt_tuning* out);
 

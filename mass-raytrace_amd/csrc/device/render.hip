@@ -98,6 +98,7 @@ struct RenderParams {
   uint32_t sample_base;  // absolute sample index of chunk sample 0
   uint32_t pool_cap;     // path slots per buffer
   const uint32_t* pixlist;
+  uint32_t shade_bin;    // k_shade: survivors grouped by material kind in the next pool (option shade_bin)
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -129,6 +130,37 @@ __device__ __forceinline__ uint32_t wg_reserve(uint32_t* counter, uint32_t count
   for (uint32_t w = 0; w < wave; ++w) base += s_cnt[w];
   __syncthreads();  // s_cnt/s_base are reused by the next call
   return base;
+}
+
+// wg_reserve for the alive lanes, the workgroup's survivors ordered by `key`
+// (< kOutKeys), then by wave and lane: returns an alive lane's slot. Used to
+// group the next pool's rays by the material kind they scattered from
+// (option shade_bin): k_trace's waves then walk rays of one kind — mirror
+// reflections, refractions, diffuse bounces — together. Every thread of the
+// workgroup must call it.
+constexpr uint32_t kOutKeys = 8;
+__device__ __forceinline__ uint32_t wg_reserve_keyed(uint32_t* counter, bool alive, uint32_t key, uint32_t wave,
+                                                     uint32_t* s_hist, uint32_t& s_base) {
+  uint32_t rank = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kOutKeys; ++k) {
+    const unsigned long long m = __ballot(alive && key == k);
+    if (lane_id() == 0) s_hist[wave * kOutKeys + k] = (uint32_t)__popcll(m);
+    if (alive && key == k) rank = lane_rank(m);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t total = 0;
+    for (uint32_t j = 0; j < kWaves * kOutKeys; ++j) total += s_hist[j];
+    s_base = total ? atomicAdd(counter, total) : 0u;
+  }
+  __syncthreads();
+  uint32_t off = s_base + rank;
+  for (uint32_t k = 0; k < kOutKeys; ++k)
+    for (uint32_t w = 0; w < kWaves; ++w)
+      if (k < key || (k == key && w < wave)) off += s_hist[w * kOutKeys + k];
+  __syncthreads();  // s_hist/s_base are reused by the next call
+  return off;
 }
 
 __device__ void flush_counters(DevCounters* c, const LocalCounters& lc, uint32_t segs, uint32_t hits,
@@ -533,7 +565,7 @@ __global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, RenderParams 
   if (blockIdx.x == 0 && threadIdx.x == 0 && n > gridDim.x * kBlock) ctrl->shade_short = n;
   LocalCounters lc;
   uint32_t nbounce = 0, nsample = 0, nshaded = 0;
-  __shared__ uint32_t s_cnt[kWaves], s_base;
+  __shared__ uint32_t s_cnt[kWaves], s_base, s_hist[kWaves * kOutKeys];
   const uint32_t wave = threadIdx.x / 64;
   {
     const uint32_t base = blockIdx.x * kBlock;
@@ -574,10 +606,17 @@ __global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, RenderParams 
     if (COUNT) shade_coherence(S, mat, lc);
     // compact the survivors into the next pool: one atomic per workgroup
     // (same-address atomics from every wave serialise in L2)
-    const unsigned long long alive_mask = __ballot(alive);
-    const uint32_t obase = wg_reserve(&ctrl->active[cur ^ 1], (uint32_t)__popcll(alive_mask), wave, s_cnt, s_base);
+    uint32_t slot;
+    if (rp.shade_bin) {  // survivors grouped by the material kind they scattered from (wg_reserve_keyed)
+      const uint32_t key = alive ? (S.materials[MRT_IDX(S, mat, S.n_materials, 4)].kind & (kOutKeys - 1)) : 0u;
+      slot = wg_reserve_keyed(&ctrl->active[cur ^ 1], alive, key, wave, s_hist, s_base);
+    } else {
+      const unsigned long long alive_mask = __ballot(alive);
+      slot = wg_reserve(&ctrl->active[cur ^ 1], (uint32_t)__popcll(alive_mask), wave, s_cnt, s_base) +
+             lane_rank(alive_mask);
+    }
     if (alive) {
-      uint32_t pos = MRT_IDX(S, obase + lane_rank(alive_mask), rp.pool_cap, 22);
+      uint32_t pos = MRT_IDX(S, slot, rp.pool_cap, 22);
       out.ro[pos] = ro;
       out.rd[pos] = rd;
       out.thr[pos] = thr;
@@ -1058,6 +1097,7 @@ enum OptId {
   OPT_TRAVERSAL,         // 0: the reference's left-first walk; 1: the verified near-first walk; -1: per scene (MRT_TRAVERSAL_*)
   OPT_TRACE_NF_BATCH,    // near-first walk: lanes whose walks are over wait for this many to check their hits together (-1: = refill)
   OPT_NF_KAPPA_LOG2,     // near-first walk: rays whose generic-triangle kappa exceeds 2^v take the reference walk (-8: every ray the bound covers)
+  OPT_SHADE_BIN,         // k_shade: group each workgroup's survivors by material kind in the next pool (0/1; -1: per scene)
   kNumOpts
 };
 struct OptDef {
@@ -1083,6 +1123,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"traversal", -1, -1, 1},
     {"trace_nf_batch", -1, -1, 64},
     {"nf_kappa_log2", -8, -40, -8},
+    {"shade_bin", -1, -1, 1},
 };
 int opt_find(const char* name) {
   if (!name) return -1;
@@ -1168,6 +1209,7 @@ struct mrt_ctx {
   bool scene_nf_gen = false;       // their rounding margin has a generic-triangle term (nf_bound.h aw1 / ko1)
   std::string nf_note;             // why it has none
   bool use_nf = false;             // k_trace walks them (option "traversal", the scene, no treelet)
+  bool shade_bin = false;          // k_shade groups its survivors by material kind (option "shade_bin")
   // LDS treelet: off by default. Measured: it removes the
   // global load of a step only when every lane of the wave is in the copy,
   // and the TA cost is per wave instruction, not per lane — 256/16 KB and
@@ -1310,6 +1352,11 @@ void apply_options(mrt_ctx* c) {
   if (c->wgs_per_cu != (uint32_t)o[OPT_TRACE_WGS_PER_CU]) c->grids.clear();
   c->wgs_per_cu = (uint32_t)o[OPT_TRACE_WGS_PER_CU];
   c->S.nfb.kmax = ldexpf(1.0f, (int)o[OPT_NF_KAPPA_LOG2]);
+  // survivors grouped by material kind (round 5, profiles/r5_shade_bin/):
+  // sphere_grid 972.1 -> 1000.8, cube_field 503.9 -> 514.0 Msamples/s (k_trace
+  // lane utilisation 0.731 -> 0.765: a wave walks rays of one kind); mesh_ply,
+  // C5, Menger within noise (one material kind dominates) — on everywhere
+  c->shade_bin = o[OPT_SHADE_BIN] != 0;
 }
 
 // Validates and stores option `id`; the caller re-derives (apply_options).
@@ -1786,6 +1833,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
     rp.sample_base = a->spp_begin + done;
     rp.pixlist = pl.first;
     rp.pool_cap = (uint32_t)c->q[0].cap;
+    rp.shade_bin = c->shade_bin ? 1u : 0u;
     if (a->max_depth == 0) {
       // trace(ray, 0) returns (0, 0) for every sample: nothing to add
       continue;
@@ -2251,6 +2299,7 @@ int mrt_get_tuning(mrt_ctx* c, mrt_tuning* out) {
     out->pool_paths = c->pool_paths;
     out->results_max = c->results_max;
     out->traversal = c->use_nf ? MRT_TRAVERSAL_NEAR_FIRST : MRT_TRAVERSAL_REFERENCE;
+    out->shade_bin = c->shade_bin ? 1u : 0u;
   });
 }
 

@@ -151,7 +151,8 @@ class MrtKernelStats(C.Structure):
 class MrtTuning(C.Structure):
     _fields_ = [("queues", C.c_uint32), ("trace_refill", C.c_uint32), ("trace_box_min", C.c_uint32),
                 ("trace_chunk", C.c_uint32), ("shade_waves", C.c_uint32), ("pool_paths", C.c_uint64),
-                ("results_max", C.c_uint64), ("traversal", C.c_uint32)]
+                ("results_max", C.c_uint64), ("traversal", C.c_uint32),
+                ("shade_bin", C.c_uint32)]
 
     def as_dict(self) -> dict:
         return {f: int(getattr(self, f)) for f, _ in self._fields_}
