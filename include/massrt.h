@@ -355,8 +355,9 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  *                     once this many lanes wait (-1: the refill threshold)
  *   shade_bin         -1, 0, 1  k_shade writes each workgroup's surviving
  *                     paths into the next pool grouped by the material kind
- *                     they scattered from, so k_trace's waves walk rays of one
- *                     kind together (-1: on); images are identical either way
+ *                     they scattered from and the signs of their direction's
+ *                     y and x, so k_trace's waves walk rays that go the same
+ *                     way together (-1: on); images are identical either way
  * Every render sizes its path pool and results slab to the device memory
  * free at that moment minus mem_reserve_mb (several contexts may share a
  * device), shrinking the pool first and then the samples per chunk. */
@@ -391,7 +392,7 @@ typedef struct {
   uint32_t queues, trace_refill, trace_box_min, trace_chunk, shade_waves;
   uint64_t pool_paths, results_max;
   uint32_t traversal; /* the walk k_trace uses for this scene (MRT_TRAVERSAL_*) */
-  uint32_t shade_bin; /* survivors grouped by material kind (option shade_bin; ABI v9) */
+  uint32_t shade_bin; /* survivors grouped by material kind and direction (option shade_bin; ABI v9) */
 } mrt_tuning;
 int mrt_get_tuning(mrt_ctx* ctx, mrt_tuning* out);
 

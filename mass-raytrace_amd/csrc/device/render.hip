@@ -98,7 +98,7 @@ struct RenderParams {
   uint32_t sample_base;  // absolute sample index of chunk sample 0
   uint32_t pool_cap;     // path slots per buffer
   const uint32_t* pixlist;
-  uint32_t shade_bin;    // k_shade: survivors grouped by material kind in the next pool (option shade_bin)
+  uint32_t shade_bin;    // k_shade: survivors grouped by material kind and direction in the next pool (option shade_bin)
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -133,34 +133,40 @@ __device__ __forceinline__ uint32_t wg_reserve(uint32_t* counter, uint32_t count
 }
 
 // wg_reserve for the alive lanes, the workgroup's survivors ordered by `key`
-// (< kOutKeys), then by wave and lane: returns an alive lane's slot. Used to
-// group the next pool's rays by the material kind they scattered from
-// (option shade_bin): k_trace's waves then walk rays of one kind — mirror
-// reflections, refractions, diffuse bounces — together. Every thread of the
-// workgroup must call it.
-constexpr uint32_t kOutKeys = 8;
-__device__ __forceinline__ uint32_t wg_reserve_keyed(uint32_t* counter, bool alive, uint32_t key, uint32_t wave,
-                                                     uint32_t* s_hist, uint32_t& s_base) {
-  uint32_t rank = 0;
+// (< kOutKeys): a lane's rank within its key comes from an LDS atomic (so
+// the order within a key is arbitrary — paths are independent, the images
+// do not depend on it), the keys' offsets from one wave's scan of the
+// histogram. k_shade uses it to group the next pool's rays by the material
+// kind they scattered from and the signs of their direction's y and x
+// (option shade_bin): k_trace's waves then walk rays that go the same way
+// together (round 5, profiles/r5_shade_bin/: kind only 1003 / 514, octant
+// 1018 / 526, kind x octant 1022 / 528, y sign only 1038 / 531, kind x y x x
+// 1035 / 535 Msamples/s on sphere_grid / cube_field, none 974 / 504). Every
+// thread of the workgroup must call it.
+constexpr uint32_t kOutKeys = 64;  // one wave scans the histogram (k_shade's keys use 32)
+__device__ __forceinline__ uint32_t wg_reserve_keyed(uint32_t* counter, bool alive, uint32_t key, uint32_t* s_hist) {
+  if (threadIdx.x < kOutKeys) s_hist[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t rank = alive ? atomicAdd(&s_hist[key], 1u) : 0u;
+  __syncthreads();
+  if (threadIdx.x < kOutKeys) {  // wave 0: exclusive scan of the 64 counts
+    const uint32_t c = s_hist[threadIdx.x];
+    uint32_t v = c;
 #pragma unroll
-  for (uint32_t k = 0; k < kOutKeys; ++k) {
-    const unsigned long long m = __ballot(alive && key == k);
-    if (lane_id() == 0) s_hist[wave * kOutKeys + k] = (uint32_t)__popcll(m);
-    if (alive && key == k) rank = lane_rank(m);
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t u = __shfl_up(v, d, 64);
+      if (lane_id() >= d) v += u;
+    }
+    const uint32_t total = __shfl(v, 63, 64);
+    uint32_t b = 0;
+    if (threadIdx.x == 0) b = total ? atomicAdd(counter, total) : 0u;
+    b = __shfl(b, 0, 64);
+    s_hist[threadIdx.x] = b + v - c;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t total = 0;
-    for (uint32_t j = 0; j < kWaves * kOutKeys; ++j) total += s_hist[j];
-    s_base = total ? atomicAdd(counter, total) : 0u;
-  }
-  __syncthreads();
-  uint32_t off = s_base + rank;
-  for (uint32_t k = 0; k < kOutKeys; ++k)
-    for (uint32_t w = 0; w < kWaves; ++w)
-      if (k < key || (k == key && w < wave)) off += s_hist[w * kOutKeys + k];
-  __syncthreads();  // s_hist/s_base are reused by the next call
-  return off;
+  const uint32_t slot = s_hist[key] + rank;
+  __syncthreads();  // s_hist is reused by the next call
+  return slot;
 }
 
 __device__ void flush_counters(DevCounters* c, const LocalCounters& lc, uint32_t segs, uint32_t hits,
@@ -565,7 +571,7 @@ __global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, RenderParams 
   if (blockIdx.x == 0 && threadIdx.x == 0 && n > gridDim.x * kBlock) ctrl->shade_short = n;
   LocalCounters lc;
   uint32_t nbounce = 0, nsample = 0, nshaded = 0;
-  __shared__ uint32_t s_cnt[kWaves], s_base, s_hist[kWaves * kOutKeys];
+  __shared__ uint32_t s_cnt[kWaves], s_base, s_hist[kOutKeys];
   const uint32_t wave = threadIdx.x / 64;
   {
     const uint32_t base = blockIdx.x * kBlock;
@@ -608,8 +614,10 @@ __global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, RenderParams 
     // (same-address atomics from every wave serialise in L2)
     uint32_t slot;
     if (rp.shade_bin) {  // survivors grouped by the material kind they scattered from (wg_reserve_keyed)
-      const uint32_t key = alive ? (S.materials[MRT_IDX(S, mat, S.n_materials, 4)].kind & (kOutKeys - 1)) : 0u;
-      slot = wg_reserve_keyed(&ctrl->active[cur ^ 1], alive, key, wave, s_hist, s_base);
+      // key: the material kind scattered from and the signs of the new ray's y and x
+      const uint32_t kind = alive ? (S.materials[MRT_IDX(S, mat, S.n_materials, 4)].kind & 7u) : 0u;
+      const uint32_t key = kind * 4u + (rd.y < 0.0f ? 2u : 0u) + (rd.x < 0.0f ? 1u : 0u);
+      slot = wg_reserve_keyed(&ctrl->active[cur ^ 1], alive, key, s_hist);
     } else {
       const unsigned long long alive_mask = __ballot(alive);
       slot = wg_reserve(&ctrl->active[cur ^ 1], (uint32_t)__popcll(alive_mask), wave, s_cnt, s_base) +
@@ -1097,7 +1105,7 @@ enum OptId {
   OPT_TRAVERSAL,         // 0: the reference's left-first walk; 1: the verified near-first walk; -1: per scene (MRT_TRAVERSAL_*)
   OPT_TRACE_NF_BATCH,    // near-first walk: lanes whose walks are over wait for this many to check their hits together (-1: = refill)
   OPT_NF_KAPPA_LOG2,     // near-first walk: rays whose generic-triangle kappa exceeds 2^v take the reference walk (-8: every ray the bound covers)
-  OPT_SHADE_BIN,         // k_shade: group each workgroup's survivors by material kind in the next pool (0/1; -1: per scene)
+  OPT_SHADE_BIN,         // k_shade: group each workgroup's survivors by material kind and direction signs (0/1; -1: on)
   kNumOpts
 };
 struct OptDef {
@@ -1209,7 +1217,7 @@ struct mrt_ctx {
   bool scene_nf_gen = false;       // their rounding margin has a generic-triangle term (nf_bound.h aw1 / ko1)
   std::string nf_note;             // why it has none
   bool use_nf = false;             // k_trace walks them (option "traversal", the scene, no treelet)
-  bool shade_bin = false;          // k_shade groups its survivors by material kind (option "shade_bin")
+  bool shade_bin = false;          // k_shade groups its survivors by material kind and direction (option "shade_bin")
   // LDS treelet: off by default. Measured: it removes the
   // global load of a step only when every lane of the wave is in the copy,
   // and the TA cost is per wave instruction, not per lane — 256/16 KB and
@@ -1352,10 +1360,10 @@ void apply_options(mrt_ctx* c) {
   if (c->wgs_per_cu != (uint32_t)o[OPT_TRACE_WGS_PER_CU]) c->grids.clear();
   c->wgs_per_cu = (uint32_t)o[OPT_TRACE_WGS_PER_CU];
   c->S.nfb.kmax = ldexpf(1.0f, (int)o[OPT_NF_KAPPA_LOG2]);
-  // survivors grouped by material kind (round 5, profiles/r5_shade_bin/):
-  // sphere_grid 972.1 -> 1000.8, cube_field 503.9 -> 514.0 Msamples/s (k_trace
-  // lane utilisation 0.731 -> 0.765: a wave walks rays of one kind); mesh_ply,
-  // C5, Menger within noise (one material kind dominates) — on everywhere
+  // survivors grouped by material kind and direction signs (round 5,
+  // profiles/r5_shade_bin/): sphere_grid 974 -> 1035, cube_field 504 -> 535
+  // Msamples/s (k_trace lane utilisation 0.731 -> 0.774: a wave walks rays
+  // that go the same way); mesh_ply, C5, Menger within noise — on everywhere
   c->shade_bin = o[OPT_SHADE_BIN] != 0;
 }
 
