@@ -111,10 +111,17 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 }
 
 constexpr uint32_t kWaves = kBlock / 64;
+// k_shade's workgroup: its survivors are grouped (option shade_bin) within
+// one workgroup, so the size sets the grouping's scope
+#ifndef MRT_SHADE_BLOCK
+#define MRT_SHADE_BLOCK 256
+#endif
+constexpr int kShadeBlock = MRT_SHADE_BLOCK;
 
 // Workgroup-wide reservation of `count` (this wave's share) consecutive
 // slots from *counter: one atomic per workgroup; returns this wave's first
 // slot. Every thread of the workgroup must call it.
+template <uint32_t NW = kWaves>
 __device__ __forceinline__ uint32_t wg_reserve(uint32_t* counter, uint32_t count, uint32_t wave, uint32_t* s_cnt,
                                                uint32_t& s_base) {
   if (lane_id() == 0) s_cnt[wave] = count;
@@ -122,7 +129,7 @@ __device__ __forceinline__ uint32_t wg_reserve(uint32_t* counter, uint32_t count
   if (threadIdx.x == 0) {
     uint32_t total = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < kWaves; ++w) total += s_cnt[w];
+    for (uint32_t w = 0; w < NW; ++w) total += s_cnt[w];
     s_base = total ? atomicAdd(counter, total) : 0u;
   }
   __syncthreads();
@@ -558,7 +565,7 @@ MRT_DEV void shade_coherence(const DevScene& S, uint32_t mat, LocalCounters& lc)
 // an L2-resident one with 8 (sphere_grid 808.8, 7: 778.1, 6: 761.0;
 // profiles/r3_tune2/wpe.txt).
 template <bool COUNT, bool EXT, int WPE>
-__global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, RenderParams rp, PathBufs in, PathBufs out,
+__global__ __launch_bounds__(kShadeBlock, WPE) void k_shade(DevScene S, RenderParams rp, PathBufs in, PathBufs out,
                                                   const uint4* hits, Ctrl* ctrl, uint32_t cur, float4* results,
                                                   DevCounters* cnt) {
   const uint32_t n = ctrl->active[cur];
@@ -568,13 +575,13 @@ __global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, RenderParams 
   // workgroup per 256 slots of the whole pool. A bound that fell short is
   // reported to the host, never dropped silently. (A grid-stride loop here
   // made the kernel spill 80 B instead of 44 and cost 3.5% of the frame.)
-  if (blockIdx.x == 0 && threadIdx.x == 0 && n > gridDim.x * kBlock) ctrl->shade_short = n;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && n > gridDim.x * kShadeBlock) ctrl->shade_short = n;
   LocalCounters lc;
   uint32_t nbounce = 0, nsample = 0, nshaded = 0;
-  __shared__ uint32_t s_cnt[kWaves], s_base, s_hist[kOutKeys];
+  __shared__ uint32_t s_cnt[kShadeBlock / 64], s_base, s_hist[kOutKeys];
   const uint32_t wave = threadIdx.x / 64;
   {
-    const uint32_t base = blockIdx.x * kBlock;
+    const uint32_t base = blockIdx.x * kShadeBlock;
     if (base >= n) return;
     const uint32_t i = base + threadIdx.x;
     bool alive = false;
@@ -620,7 +627,7 @@ __global__ __launch_bounds__(kBlock, WPE) void k_shade(DevScene S, RenderParams 
       slot = wg_reserve_keyed(&ctrl->active[cur ^ 1], alive, key, s_hist);
     } else {
       const unsigned long long alive_mask = __ballot(alive);
-      slot = wg_reserve(&ctrl->active[cur ^ 1], (uint32_t)__popcll(alive_mask), wave, s_cnt, s_base) +
+      slot = wg_reserve<kShadeBlock / 64>(&ctrl->active[cur ^ 1], (uint32_t)__popcll(alive_mask), wave, s_cnt, s_base) +
              lane_rank(alive_mask);
     }
     if (alive) {
@@ -1550,7 +1557,7 @@ void launch_trace(mrt_ctx* c, hipStream_t st, const Queue& q, const PathBufs& in
 // workgroups instead of one per 256 slots of the whole pool.
 uint32_t shade_grid(const Queue& q, size_t bound) {
   const size_t n = std::min(q.cap, bound);
-  return (uint32_t)std::max<size_t>(1, (n + kBlock - 1) / kBlock);
+  return (uint32_t)std::max<size_t>(1, (n + kShadeBlock - 1) / kShadeBlock);
 }
 
 // device bytes of a pool of P paths over the context's queues: two state
@@ -1919,7 +1926,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
             m[1] = next_event();
             HIP_CHECK(hipEventRecord(m[1], q.stream));
           }
-          hipLaunchKernelGGL(shade, dim3(shade_grid(q, L.bound)), dim3(kBlock), 0, q.stream, c->S, rp, q.bufs[cur],
+          hipLaunchKernelGGL(shade, dim3(shade_grid(q, L.bound)), dim3(kShadeBlock), 0, q.stream, c->S, rp, q.bufs[cur],
                              q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, res, c->d_cnt);
           HIP_CHECK(hipGetLastError());
           if (!L.exhausted) {  // new paths behind the survivors
