@@ -353,11 +353,17 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  *                     (nf_bound.h) exceeds 2^v take the reference walk (-8)
  *   trace_nf_batch    -1, 1..64  NEAR_FIRST: finished walks checked together
  *                     once this many lanes wait (-1: the refill threshold)
- *   shade_bin         -1, 0, 1  k_shade writes each workgroup's surviving
+ *   shade_bin      -1, 0, 1, 2  k_shade writes each workgroup's surviving
  *                     paths into the next pool grouped by the material kind
  *                     they scattered from and the signs of their direction's
  *                     y and x, so k_trace's waves walk rays that go the same
- *                     way together (-1: on); images are identical either way
+ *                     way together (1); 2 also splits the whole pool by the
+ *                     y sign (up-going paths from the bottom, down-going from
+ *                     the top, new camera rays between); -1: 2 under the
+ *                     near-first walk, 1 under the reference walk (round 5:
+ *                     sphere_grid 974 / 1030 / 1068 Msamples/s at 0 / 1 / 2,
+ *                     mesh_ply 1149 / 1151 / 1134); images are identical
+ *                     whichever is set
  * Every render sizes its path pool and results slab to the device memory
  * free at that moment minus mem_reserve_mb (several contexts may share a
  * device), shrinking the pool first and then the samples per chunk. */
@@ -392,7 +398,7 @@ typedef struct {
   uint32_t queues, trace_refill, trace_box_min, trace_chunk, shade_waves;
   uint64_t pool_paths, results_max;
   uint32_t traversal; /* the walk k_trace uses for this scene (MRT_TRAVERSAL_*) */
-  uint32_t shade_bin; /* survivors grouped by material kind and direction (option shade_bin; ABI v9) */
+  uint32_t shade_bin; /* 0, 1, 2: the survivor grouping in effect (option shade_bin; ABI v9) */
 } mrt_tuning;
 int mrt_get_tuning(mrt_ctx* ctx, mrt_tuning* out);
 

@@ -60,7 +60,13 @@ struct Ctrl {
   // refill (k_reserve -> k_refill): work items [gen_base, gen_base + gen_count)
   // go to pool slots [gen_slot, gen_slot + gen_count), behind the survivors
   uint32_t gen_slot, gen_count, gen_base;
-  uint32_t pad_[25];
+  // shade_bin 2: survivors of the second half of the keys count from the top
+  // of the next pool (active_hi); k_reserve then closes the gap between the
+  // two ends that the refill leaves: k_refill moves gen_move paths from
+  // gen_move_src.. to gen_move_dst..
+  uint32_t active_hi[2];
+  uint32_t gen_move, gen_move_src, gen_move_dst;
+  uint32_t pad_[20];
   // persistent k_trace work counters (zeroed by k_shade), one 128-B line per
   // XCD group: group g takes its rays from the g-th eighth of the pool
   uint32_t group_next[kGroups * 32];
@@ -151,7 +157,12 @@ __device__ __forceinline__ uint32_t wg_reserve(uint32_t* counter, uint32_t count
 // 1035 / 535 Msamples/s on sphere_grid / cube_field, none 974 / 504). Every
 // thread of the workgroup must call it.
 constexpr uint32_t kOutKeys = 64;  // one wave scans the histogram (k_shade's keys use 32)
-__device__ __forceinline__ uint32_t wg_reserve_keyed(uint32_t* counter, bool alive, uint32_t key, uint32_t* s_hist) {
+// hi != nullptr (shade_bin 2): keys >= 32 take slots counted down from the
+// top of the pool (cap - 1, cap - 2, ...) from *hi instead: the next pool
+// then holds the two halves at its two ends, and k_reserve/k_refill put the
+// new camera rays between them.
+__device__ __forceinline__ uint32_t wg_reserve_keyed(uint32_t* counter, bool alive, uint32_t key, uint32_t* s_hist,
+                                                     uint32_t* hi = nullptr, uint32_t cap = 0) {
   if (threadIdx.x < kOutKeys) s_hist[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t rank = alive ? atomicAdd(&s_hist[key], 1u) : 0u;
@@ -165,13 +176,18 @@ __device__ __forceinline__ uint32_t wg_reserve_keyed(uint32_t* counter, bool ali
       if (lane_id() >= d) v += u;
     }
     const uint32_t total = __shfl(v, 63, 64);
-    uint32_t b = 0;
-    if (threadIdx.x == 0) b = total ? atomicAdd(counter, total) : 0u;
+    const uint32_t tlo = hi ? __shfl(v, 31, 64) : total, thi = total - tlo;
+    uint32_t b = 0, bh = 0;
+    if (threadIdx.x == 0) {
+      b = tlo ? atomicAdd(counter, tlo) : 0u;
+      if (thi) bh = atomicAdd(hi, thi);
+    }
     b = __shfl(b, 0, 64);
-    s_hist[threadIdx.x] = b + v - c;
+    bh = __shfl(bh, 0, 64);
+    s_hist[threadIdx.x] = hi && threadIdx.x >= 32 ? cap - 1u - bh - (v - c - tlo) : b + v - c;
   }
   __syncthreads();
-  const uint32_t slot = s_hist[key] + rank;
+  const uint32_t slot = hi && key >= 32 ? s_hist[key] - rank : s_hist[key] + rank;
   __syncthreads();  // s_hist is reused by the next call
   return slot;
 }
@@ -246,17 +262,25 @@ __global__ void k_status(const Ctrl* ctrl, const uint32_t* work, HostStatus* out
 // advanced while it is below G, so it passes G by at most a pool per queue.
 __global__ void k_reserve(Ctrl* ctrl, uint32_t cur, uint32_t* work, uint32_t G, uint32_t cap) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const uint32_t n = ctrl->active[cur ^ 1];
+  const uint32_t lo = ctrl->active[cur ^ 1], hi = ctrl->active_hi[cur ^ 1], n = lo + hi;
   const uint32_t want = n < cap ? cap - n : 0u;
   uint32_t m = 0, base = G;
   if (want && __hip_atomic_load(work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G) {
     base = atomicAdd(work, want);
     m = base < G ? (G - base < want ? G - base : want) : 0u;
   }
-  ctrl->gen_slot = n;
+  ctrl->gen_slot = lo;
   ctrl->gen_count = m;
   ctrl->gen_base = base;
-  ctrl->active[cur ^ 1] = n + m;
+  // the top block [cap - hi, cap) closes onto the refill's end lo + m: its
+  // paths at or past the new end E move into the free slots below E
+  const uint32_t E = n + m, g = cap - E;
+  const uint32_t mv = g < hi ? g : hi;
+  ctrl->gen_move = mv;
+  ctrl->gen_move_src = cap - mv;
+  ctrl->gen_move_dst = lo + m;
+  ctrl->active[cur ^ 1] = E;
+  ctrl->active_hi[cur ^ 1] = 0;
 }
 
 // ... and generate them (camera rays of consecutive work items, i.e. pixel
@@ -264,6 +288,17 @@ __global__ void k_reserve(Ctrl* ctrl, uint32_t cur, uint32_t* work, uint32_t G, 
 // survivors instead of scattered among them one per finished slot.
 __global__ __launch_bounds__(kBlock) void k_refill(DevCamera cam, RenderParams rp, PathBufs out, const Ctrl* ctrl) {
   const uint32_t m = ctrl->gen_count, slot = ctrl->gen_slot, base = ctrl->gen_base;
+  const uint32_t mv = ctrl->gen_move, src = ctrl->gen_move_src, dst = ctrl->gen_move_dst;
+  for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < mv; j += gridDim.x * kBlock) {
+    // sources [cap - mv, cap) and destinations [lo + m, lo + m + mv) are disjoint
+    const uint32_t a = src + j, b = dst + j;
+    const float4 thr = out.thr[a];
+    out.ro[b] = out.ro[a];
+    out.rd[b] = out.rd[a];
+    out.thr[b] = thr;
+    if (holds_l(thr)) out.rad[b] = out.rad[a];
+    out.rng[b] = out.rng[a];
+  }
   for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < m; j += gridDim.x * kBlock) {
     float4 ro, rd;
     uint4 rs;
@@ -319,7 +354,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(NF ? (COUNT
   static_assert(!NF || (!LDS && !RNG), "the near-first walk has no treelet and no traversal draws");
   constexpr int R = 1;
   const uint32_t n = ctrl->active[cur];
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = ctrl->active_hi[cur ^ 1] = 0;
   if (n == 0) return;  // uniform: every workgroup reads the same n
   if (LDS) {
     for (uint32_t k = threadIdx.x; k < S.n_tlet; k += BLK) mrt_lds[k] = reinterpret_cast<const uint4*>(S.tlet)[k];
@@ -481,7 +516,7 @@ template <bool RNG>
 __global__ __launch_bounds__(kBlock) void k_trace_simple(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl,
                                                          uint32_t cur, DevCounters* cnt) {
   const uint32_t n = ctrl->active[cur];
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = ctrl->active_hi[cur ^ 1] = 0;
   LocalCounters lc;
   uint32_t seg = 0, nh = 0;
   const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), S.world_begin, in.ro, in.rd, kTmin, in.rng};
@@ -623,8 +658,13 @@ __global__ __launch_bounds__(kShadeBlock, WPE) void k_shade(DevScene S, RenderPa
     if (rp.shade_bin) {  // survivors grouped by the material kind they scattered from (wg_reserve_keyed)
       // key: the material kind scattered from and the signs of the new ray's y and x
       const uint32_t kind = alive ? (S.materials[MRT_IDX(S, mat, S.n_materials, 4)].kind & 7u) : 0u;
-      const uint32_t key = kind * 4u + (rd.y < 0.0f ? 2u : 0u) + (rd.x < 0.0f ? 1u : 0u);
-      slot = wg_reserve_keyed(&ctrl->active[cur ^ 1], alive, key, s_hist);
+      if (rp.shade_bin == 2) {  // y sign: the two ends of the pool; kind and x, z signs within
+        const uint32_t key = (rd.y < 0.0f ? 32u : 0u) + kind * 4u + (rd.x < 0.0f ? 2u : 0u) + (rd.z < 0.0f ? 1u : 0u);
+        slot = wg_reserve_keyed(&ctrl->active[cur ^ 1], alive, key, s_hist, &ctrl->active_hi[cur ^ 1], rp.pool_cap);
+      } else {
+        const uint32_t key = kind * 4u + (rd.y < 0.0f ? 2u : 0u) + (rd.x < 0.0f ? 1u : 0u);
+        slot = wg_reserve_keyed(&ctrl->active[cur ^ 1], alive, key, s_hist);
+      }
     } else {
       const unsigned long long alive_mask = __ballot(alive);
       slot = wg_reserve<kShadeBlock / 64>(&ctrl->active[cur ^ 1], (uint32_t)__popcll(alive_mask), wave, s_cnt, s_base) +
@@ -1112,7 +1152,7 @@ enum OptId {
   OPT_TRAVERSAL,         // 0: the reference's left-first walk; 1: the verified near-first walk; -1: per scene (MRT_TRAVERSAL_*)
   OPT_TRACE_NF_BATCH,    // near-first walk: lanes whose walks are over wait for this many to check their hits together (-1: = refill)
   OPT_NF_KAPPA_LOG2,     // near-first walk: rays whose generic-triangle kappa exceeds 2^v take the reference walk (-8: every ray the bound covers)
-  OPT_SHADE_BIN,         // k_shade: group each workgroup's survivors by material kind and direction signs (0/1; -1: on)
+  OPT_SHADE_BIN,         // k_shade: group each workgroup's survivors by material kind and direction signs (1), and split the pool by y sign (2); -1: per scene
   kNumOpts
 };
 struct OptDef {
@@ -1138,7 +1178,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"traversal", -1, -1, 1},
     {"trace_nf_batch", -1, -1, 64},
     {"nf_kappa_log2", -8, -40, -8},
-    {"shade_bin", -1, -1, 1},
+    {"shade_bin", -1, -1, 2},
 };
 int opt_find(const char* name) {
   if (!name) return -1;
@@ -1224,7 +1264,7 @@ struct mrt_ctx {
   bool scene_nf_gen = false;       // their rounding margin has a generic-triangle term (nf_bound.h aw1 / ko1)
   std::string nf_note;             // why it has none
   bool use_nf = false;             // k_trace walks them (option "traversal", the scene, no treelet)
-  bool shade_bin = false;          // k_shade groups its survivors by material kind and direction (option "shade_bin")
+  int shade_bin = 0;                        // k_shade groups its survivors by material kind and direction (option "shade_bin")
   // LDS treelet: off by default. Measured: it removes the
   // global load of a step only when every lane of the wave is in the copy,
   // and the TA cost is per wave instruction, not per lane — 256/16 KB and
@@ -1370,8 +1410,11 @@ void apply_options(mrt_ctx* c) {
   // survivors grouped by material kind and direction signs (round 5,
   // profiles/r5_shade_bin/): sphere_grid 974 -> 1035, cube_field 504 -> 535
   // Msamples/s (k_trace lane utilisation 0.731 -> 0.774: a wave walks rays
-  // that go the same way); mesh_ply, C5, Menger within noise — on everywhere
-  c->shade_bin = o[OPT_SHADE_BIN] != 0;
+  // that go the same way); mesh_ply, C5, Menger within noise. The pool-wide
+  // y-sign split (2) on top: sphere_grid 1030 -> 1068, cube_field 537 -> 555
+  // (utilisation 0.774 -> 0.798), but mesh_ply 1151 -> 1134
+  // (profiles/r5_shade_block/) — 2 where the near-first walk runs, else 1
+  c->shade_bin = o[OPT_SHADE_BIN] >= 0 ? (int)o[OPT_SHADE_BIN] : (nf ? 2 : 1);
 }
 
 // Validates and stores option `id`; the caller re-derives (apply_options).
@@ -1848,7 +1891,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
     rp.sample_base = a->spp_begin + done;
     rp.pixlist = pl.first;
     rp.pool_cap = (uint32_t)c->q[0].cap;
-    rp.shade_bin = c->shade_bin ? 1u : 0u;
+    rp.shade_bin = (uint32_t)c->shade_bin;
     if (a->max_depth == 0) {
       // trace(ray, 0) returns (0, 0) for every sample: nothing to add
       continue;
@@ -1929,7 +1972,7 @@ void render_device(mrt_ctx* c, const mrt_render_args* a, float* d_rgb, uint32_t*
           hipLaunchKernelGGL(shade, dim3(shade_grid(q, L.bound)), dim3(kShadeBlock), 0, q.stream, c->S, rp, q.bufs[cur],
                              q.bufs[cur ^ 1], (const uint4*)q.hits, q.ctrl, cur, res, c->d_cnt);
           HIP_CHECK(hipGetLastError());
-          if (!L.exhausted) {  // new paths behind the survivors
+          if (!L.exhausted || rp.shade_bin == 2) {  // new paths behind the survivors (shade_bin 2: and the pool's ends joined)
             hipLaunchKernelGGL(k_reserve, dim3(1), dim3(64), 0, q.stream, q.ctrl, cur, work, rp.G, rp.pool_cap);
             hipLaunchKernelGGL(k_refill, dim3(c->refill_grid), dim3(kBlock), 0, q.stream, c->cam, rp, q.bufs[cur ^ 1],
                                (const Ctrl*)q.ctrl);
@@ -2314,7 +2357,7 @@ int mrt_get_tuning(mrt_ctx* c, mrt_tuning* out) {
     out->pool_paths = c->pool_paths;
     out->results_max = c->results_max;
     out->traversal = c->use_nf ? MRT_TRAVERSAL_NEAR_FIRST : MRT_TRAVERSAL_REFERENCE;
-    out->shade_bin = c->shade_bin ? 1u : 0u;
+    out->shade_bin = (uint32_t)c->shade_bin;
   });
 }
 

@@ -113,23 +113,27 @@ def test_shading_coherence_counters(scene, golden_dir):
 @pytest.mark.parametrize("finish", [0, None])
 def test_shade_bin_is_bit_identical(scene, golden_dir, finish):
     """Option shade_bin: k_shade writes each workgroup's survivors into the
-    next pool grouped by the material kind they scattered from. Paths are
+    next pool grouped by the material kind they scattered from (1), or split
+    by the new ray's y sign between the pool's two ends (2). Paths are
     independent, so the image is the ungrouped one bit for bit (with and
-    without the drain hand-off), and so is the work counted."""
+    without the drain hand-off), and so is the work counted. A 64K-path pool
+    makes the 236K samples refill it (2: the refill between the two ends, and
+    the gap closed once the work runs out)."""
     for src in (scene, massrt.Builder(1).builtin("cube_field", ASPECT, golden_dir)):
         out, cnt = [], []
-        for b in (0, 1):
-            opts = {"shade_bin": b, **({"finish_paths": finish} if finish is not None else {})}
+        for b in (0, 1, 2):
+            opts = {"shade_bin": b, "pool_paths": 1 << 16, **({"finish_paths": finish} if finish is not None else {})}
             c = massrt.Context(0, options=opts)
             c.upload(src)
-            out.append(c.render(W, H, 0, 6, seed=13))
+            out.append(c.render(W, H, 0, 24, seed=13))
             c.reset_counters()
             c.render(W, H, 0, 2, seed=13, counters=True)
             cnt.append(c.counters())
             c.close()
-        assert _same(out[0][0], out[1][0]) and _same(out[0][1], out[1][1])
-        for k in ("samples", "segments", "bounces", "shaded", "closest_hits"):
-            assert cnt[0][k] == cnt[1][k], k
+        for j in (1, 2):
+            assert _same(out[0][0], out[j][0]) and _same(out[0][1], out[j][1]), j
+            for k in ("samples", "segments", "bounces", "shaded", "closest_hits"):
+                assert cnt[0][k] == cnt[j][k], (j, k)
 
 
 @pytest.mark.parametrize("devices", [[0, 0, 0], [0]])
@@ -237,13 +241,14 @@ def test_options_and_tuning(scene, golden_dir):
     # traversal AUTO: sphere_grid takes the near-first walk (its own rules: refill 40, k_shade at 7)
     assert c.get_option("traversal") == massrt.TRAVERSAL_AUTO and t["traversal"] == massrt.TRAVERSAL_NEAR_FIRST
     assert t["queues"] == 2 and t["trace_box_min"] == 24 and t["trace_chunk"] == 512 and t["shade_waves"] == 7
-    assert t["shade_bin"] == 1 and c.get_option("shade_bin") == -1  # survivors grouped by material kind (on)
+    assert t["shade_bin"] == 2 and c.get_option("shade_bin") == -1  # grouped survivors, pool split by y sign (near-first)
     c.set_option("shade_bin", 0)
     assert c.tuning()["shade_bin"] == 0
     c.set_option("shade_bin", -1)
     c.set_option("traversal", massrt.TRAVERSAL_REFERENCE)
     t = c.tuning()
     assert t["traversal"] == massrt.TRAVERSAL_REFERENCE and t["trace_refill"] == 32 and t["shade_waves"] == 8
+    assert t["shade_bin"] == 1  # the reference walk: grouped survivors, no pool split
     c.set_option("traversal", massrt.TRAVERSAL_NEAR_FIRST)  # its own rules: refill 40, k_shade at 7
     t = c.tuning()
     assert t["traversal"] == massrt.TRAVERSAL_NEAR_FIRST and t["trace_refill"] == 40 and t["shade_waves"] == 7
