@@ -57,16 +57,20 @@ struct Ctrl {
   uint32_t active[2];
   uint32_t next_work;
   uint32_t shade_short;  // nonzero: a k_shade grid did not cover its live pool (host bound wrong; reported)
+  // shade_bin 2: the survivors of the first half of the keys counted from the
+  // bottom of the next pool (low word) and of the second half from its top
+  // (high word), in one 64-bit word so that a workgroup reserves both with
+  // ONE atomic (two, one per word, doubled k_shade's solo time: every
+  // workgroup's atomics go to this one line)
+  unsigned long long surv[2];
   // refill (k_reserve -> k_refill): work items [gen_base, gen_base + gen_count)
   // go to pool slots [gen_slot, gen_slot + gen_count), behind the survivors
   uint32_t gen_slot, gen_count, gen_base;
-  // shade_bin 2: survivors of the second half of the keys count from the top
-  // of the next pool (active_hi); k_reserve then closes the gap between the
-  // two ends that the refill leaves: k_refill moves gen_move paths from
-  // gen_move_src.. to gen_move_dst..
-  uint32_t active_hi[2];
+  // shade_bin 2: k_reserve closes the gap between the pool's two ends that
+  // the refill leaves: k_refill moves gen_move paths from gen_move_src.. to
+  // gen_move_dst..
   uint32_t gen_move, gen_move_src, gen_move_dst;
-  uint32_t pad_[20];
+  uint32_t pad_[18];
   // persistent k_trace work counters (zeroed by k_shade), one 128-B line per
   // XCD group: group g takes its rays from the g-th eighth of the pool
   uint32_t group_next[kGroups * 32];
@@ -158,11 +162,12 @@ __device__ __forceinline__ uint32_t wg_reserve(uint32_t* counter, uint32_t count
 // thread of the workgroup must call it.
 constexpr uint32_t kOutKeys = 64;  // one wave scans the histogram (k_shade's keys use 32)
 // hi != nullptr (shade_bin 2): keys >= 32 take slots counted down from the
-// top of the pool (cap - 1, cap - 2, ...) from *hi instead: the next pool
-// then holds the two halves at its two ends, and k_reserve/k_refill put the
-// new camera rays between them.
+// top of the pool (cap - 1, cap - 2, ...) instead: both counts go to *hi
+// (low word: from the bottom, high word: from the top, one atomic; *counter
+// is unused), the next pool then holds the two halves at its two ends, and
+// k_reserve/k_refill put the new camera rays between them.
 __device__ __forceinline__ uint32_t wg_reserve_keyed(uint32_t* counter, bool alive, uint32_t key, uint32_t* s_hist,
-                                                     uint32_t* hi = nullptr, uint32_t cap = 0) {
+                                                     unsigned long long* hi = nullptr, uint32_t cap = 0) {
   if (threadIdx.x < kOutKeys) s_hist[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t rank = alive ? atomicAdd(&s_hist[key], 1u) : 0u;
@@ -179,8 +184,13 @@ __device__ __forceinline__ uint32_t wg_reserve_keyed(uint32_t* counter, bool ali
     const uint32_t tlo = hi ? __shfl(v, 31, 64) : total, thi = total - tlo;
     uint32_t b = 0, bh = 0;
     if (threadIdx.x == 0) {
-      b = tlo ? atomicAdd(counter, tlo) : 0u;
-      if (thi) bh = atomicAdd(hi, thi);
+      if (hi) {
+        const unsigned long long r = total ? atomicAdd(hi, ((unsigned long long)thi << 32) | tlo) : 0ull;
+        b = (uint32_t)r;
+        bh = (uint32_t)(r >> 32);
+      } else {
+        b = total ? atomicAdd(counter, total) : 0u;
+      }
     }
     b = __shfl(b, 0, 64);
     bh = __shfl(bh, 0, 64);
@@ -262,7 +272,8 @@ __global__ void k_status(const Ctrl* ctrl, const uint32_t* work, HostStatus* out
 // advanced while it is below G, so it passes G by at most a pool per queue.
 __global__ void k_reserve(Ctrl* ctrl, uint32_t cur, uint32_t* work, uint32_t G, uint32_t cap) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const uint32_t lo = ctrl->active[cur ^ 1], hi = ctrl->active_hi[cur ^ 1], n = lo + hi;
+  const unsigned long long sv = ctrl->surv[cur ^ 1];  // 0 unless shade_bin 2
+  const uint32_t lo = ctrl->active[cur ^ 1] + (uint32_t)sv, hi = (uint32_t)(sv >> 32), n = lo + hi;
   const uint32_t want = n < cap ? cap - n : 0u;
   uint32_t m = 0, base = G;
   if (want && __hip_atomic_load(work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G) {
@@ -280,7 +291,7 @@ __global__ void k_reserve(Ctrl* ctrl, uint32_t cur, uint32_t* work, uint32_t G, 
   ctrl->gen_move_src = cap - mv;
   ctrl->gen_move_dst = lo + m;
   ctrl->active[cur ^ 1] = E;
-  ctrl->active_hi[cur ^ 1] = 0;
+  ctrl->surv[cur ^ 1] = 0;
 }
 
 // ... and generate them (camera rays of consecutive work items, i.e. pixel
@@ -354,7 +365,10 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(NF ? (COUNT
   static_assert(!NF || (!LDS && !RNG), "the near-first walk has no treelet and no traversal draws");
   constexpr int R = 1;
   const uint32_t n = ctrl->active[cur];
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = ctrl->active_hi[cur ^ 1] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ctrl->active[cur ^ 1] = 0;
+    ctrl->surv[cur ^ 1] = 0;
+  }
   if (n == 0) return;  // uniform: every workgroup reads the same n
   if (LDS) {
     for (uint32_t k = threadIdx.x; k < S.n_tlet; k += BLK) mrt_lds[k] = reinterpret_cast<const uint4*>(S.tlet)[k];
@@ -516,7 +530,10 @@ template <bool RNG>
 __global__ __launch_bounds__(kBlock) void k_trace_simple(DevScene S, PathBufs in, uint4* hits, Ctrl* ctrl,
                                                          uint32_t cur, DevCounters* cnt) {
   const uint32_t n = ctrl->active[cur];
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->active[cur ^ 1] = ctrl->active_hi[cur ^ 1] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ctrl->active[cur ^ 1] = 0;
+    ctrl->surv[cur ^ 1] = 0;
+  }
   LocalCounters lc;
   uint32_t seg = 0, nh = 0;
   const TravIn tin{S, reinterpret_cast<const uint4*>(S.slots), S.world_begin, in.ro, in.rd, kTmin, in.rng};
@@ -660,7 +677,7 @@ __global__ __launch_bounds__(kShadeBlock, WPE) void k_shade(DevScene S, RenderPa
       const uint32_t kind = alive ? (S.materials[MRT_IDX(S, mat, S.n_materials, 4)].kind & 7u) : 0u;
       if (rp.shade_bin == 2) {  // y sign: the two ends of the pool; kind and x, z signs within
         const uint32_t key = (rd.y < 0.0f ? 32u : 0u) + kind * 4u + (rd.x < 0.0f ? 2u : 0u) + (rd.z < 0.0f ? 1u : 0u);
-        slot = wg_reserve_keyed(&ctrl->active[cur ^ 1], alive, key, s_hist, &ctrl->active_hi[cur ^ 1], rp.pool_cap);
+        slot = wg_reserve_keyed(&ctrl->active[cur ^ 1], alive, key, s_hist, &ctrl->surv[cur ^ 1], rp.pool_cap);
       } else {
         const uint32_t key = kind * 4u + (rd.y < 0.0f ? 2u : 0u) + (rd.x < 0.0f ? 1u : 0u);
         slot = wg_reserve_keyed(&ctrl->active[cur ^ 1], alive, key, s_hist);
@@ -1411,9 +1428,11 @@ void apply_options(mrt_ctx* c) {
   // profiles/r5_shade_bin/): sphere_grid 974 -> 1035, cube_field 504 -> 535
   // Msamples/s (k_trace lane utilisation 0.731 -> 0.774: a wave walks rays
   // that go the same way); mesh_ply, C5, Menger within noise. The pool-wide
-  // y-sign split (2) on top: sphere_grid 1030 -> 1068, cube_field 537 -> 555
-  // (utilisation 0.774 -> 0.798), but mesh_ply 1151 -> 1134
-  // (profiles/r5_shade_block/) — 2 where the near-first walk runs, else 1
+  // y-sign split (2) on top, its two counts in one 64-bit atomic per
+  // workgroup: sphere_grid 1035 -> 1086, cube_field 538 -> 558 (utilisation
+  // 0.774 -> 0.798), mesh_ply 1150 -> 1152, C5 1137 -> 1132
+  // (profiles/r5_surv64/; with two 32-bit atomics mesh_ply lost 1151 -> 1134,
+  // profiles/r5_shade_block/) — 2 where the near-first walk runs, else 1
   c->shade_bin = o[OPT_SHADE_BIN] >= 0 ? (int)o[OPT_SHADE_BIN] : (nf ? 2 : 1);
 }
 
