@@ -2,11 +2,12 @@
 # shade_bin 2 with both survivor counts in one 64-bit atomic per workgroup
 # (two 32-bit atomics doubled k_shade's solo time): parity, then shade_bin
 # 1 vs 2 on the bench scenes, two queues and solo.
-# The variant library: profiles/r5_experiments/surv64.patch built as
-# massrt/libmassrt_surv64.so (make OUT=massrt/libmassrt_surv64.so BUILD=build_surv64).
+# Measured (profiles/r5_surv64/) with profiles/r5_experiments/surv64.patch
+# built as a variant library (MASSRT_LIB=mass-raytrace_amd/massrt/libmassrt_surv64.so,
+# make OUT=massrt/libmassrt_surv64.so BUILD=build_surv64); the patch is in
+# the source since, so the script now measures the default library.
 set -o pipefail
 export TMPDIR=/tmp
-export MASSRT_LIB=mass-raytrace_amd/massrt/libmassrt_surv64.so
 mkdir -p gpurun_out/session
 timeout -k 10 300 python -u -m pytest tests/test_gpu_frames.py -x -q --timeout 120 --timeout-method thread -k "shade_bin or options" \
   > gpurun_out/session/pytest_bin.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/session/pytest_bin.log; exit 1; }
