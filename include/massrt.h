@@ -448,8 +448,9 @@ int mrt_context_devices(mrt_ctx* ctx, int* n_devices, int* devices);
 /* the gather transport: "none" (one device), "peer", "rccl", or
  * "peer (...)" with the reason RCCL was not used */
 const char* mrt_context_transport(const mrt_ctx* ctx);
-/* Test hooks of the transport choice (no GPU needed): the library RCCL is
- * opened from (NULL or "": librccl.so.1), and the transport
+/* TEST-ONLY hooks of the transport choice (no GPU needed): the library RCCL
+ * is opened from (NULL or "": librccl.so.1) by contexts created after the
+ * call (a live context keeps the RCCL it was created with), and the transport
  * mrt_create_multi would pick for these devices — opening RCCL but creating
  * no communicators — written to buf (e.g. "peer (RCCL unavailable: ...)"). */
 int mrt_debug_rccl_library(const char* name);
@@ -493,10 +494,6 @@ int mrt_image_gather_stats(mrt_image* img, uint64_t* bytes, double* ms);
 /* per-device render time so far (ms, HIP events around each device's share
  * of every mrt_image_render; waits for renders still running); render_ms has
  * one entry per device of the context */
-int mrt_image_device_stats(mrt_image* img, int n_devices, double* render_ms);
-/* per-device render time so far (ms, HIP events around each device's share
- * of every mrt_image_render; waits for renders still running); render_ms has
- * one entry per device of the context (ABI v8 addition) */
 int mrt_image_device_stats(mrt_image* img, int n_devices, double* render_ms);
 
 /* ---- build identity (ABI v7) -------------------------------------------

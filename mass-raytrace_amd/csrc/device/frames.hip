@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -66,16 +67,19 @@ struct Rccl {
 };
 
 // the library RCCL is opened from (mrt_debug_rccl_library: a test points it
-// at a missing file to take the peer-copy fallback on a machine that has RCCL)
+// at a missing file to take the peer-copy fallback on a machine that has RCCL).
+// One table per library name, loaded once and never overwritten: a context
+// keeps the table it was created with (MultiDev::R), so the test hook never
+// changes the function pointers a live context is calling through.
 std::string g_rccl_name = "librccl.so.1";
-bool g_rccl_tried = false;
+std::map<std::string, std::unique_ptr<Rccl>> g_rccl_tables;
 std::mutex g_rccl_mu;
 const Rccl& rccl() {
-  static Rccl r;
   std::lock_guard<std::mutex> lk(g_rccl_mu);
-  if (!g_rccl_tried) {
-    g_rccl_tried = true;
-    r = Rccl{};
+  std::unique_ptr<Rccl>& slot = g_rccl_tables[g_rccl_name];
+  if (!slot) {
+    slot.reset(new Rccl{});
+    Rccl& r = *slot;
     void* h = dlopen(g_rccl_name.c_str(), RTLD_NOW | RTLD_LOCAL);
     if (!h && g_rccl_name == "librccl.so.1") h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
     if (h) {
@@ -88,6 +92,7 @@ const Rccl& rccl() {
       r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
     }
   }
+  const Rccl& r = *slot;
   if (!r.comm_init_all || !r.group_start || !r.group_end || !r.send || !r.recv || !r.error_string)
     throw Fail{MRT_ERR_HIP, "RCCL (" + g_rccl_name + ") is not available"};
   return r;
@@ -96,7 +101,7 @@ const Rccl& rccl() {
 #define NCCLF(x)                                                                                     \
   do {                                                                                               \
     ncclResult_t r_ = (x);                                                                           \
-    if (r_ != ncclSuccess) throw Fail{MRT_ERR_HIP, std::string(#x) + ": " + rccl().error_string(r_)}; \
+    if (r_ != ncclSuccess) throw Fail{MRT_ERR_HIP, std::string(#x) + ": " + m->R->error_string(r_)}; \
   } while (0)
 
 bool valid_size(uint32_t W, uint32_t H) { return W && H && (uint64_t)W * H < (1ull << 32); }
@@ -119,6 +124,26 @@ struct DevFrame {
   // (mrt_image_device_stats collects them; a render never waits for them)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
   double render_ms = 0;  // this device's render time so far (HIP events)
+  // past kMaxPending pairs (a caller that never reads the stats, e.g. the
+  // drop-in render() loop) the finished ones are folded into render_ms, so
+  // the list stays bounded without making a render wait (the caller's device
+  // is current)
+  static constexpr size_t kMaxPending = 64;
+  void fold_finished() {
+    if (pending.size() < kMaxPending) return;
+    size_t keep = 0;
+    for (size_t k = 0; k < pending.size(); ++k) {
+      auto& e = pending[k];
+      float ms = 0;
+      if (hipEventQuery(e.second) == hipSuccess && hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) {
+        render_ms += ms;
+        hipEventDestroy(e.first), hipEventDestroy(e.second);
+      } else {
+        pending[keep++] = e;
+      }
+    }
+    pending.resize(keep);
+  }
 };
 
 // A frame over the devices of a context: device i owns shard si + i*sc of sc*n.
@@ -194,6 +219,7 @@ struct Frame {
     auto one = [&](size_t i, mrt_render_args a) {
       DevFrame& f = d[i];
       HIPF(hipSetDevice(f.device));
+      f.fold_finished();
       hipEvent_t e0 = nullptr, e1 = nullptr;
       HIPF(hipEventCreate(&e0));
       HIPF(hipEventCreate(&e1));
@@ -257,6 +283,7 @@ struct MultiDev {
   int64_t mode = MRT_GATHER_AUTO;
   std::string transport = "peer";
   std::vector<ncclComm_t> comms;  // created with the context (distinct devices)
+  const Rccl* R = nullptr;        // the RCCL table the communicators were created with
   Frame* scratch = nullptr;       // mrt_render's frame (host buffers)
 };
 
@@ -265,7 +292,8 @@ namespace {
 void ensure_comms(MultiDev* m) {
   if (!m->comms.empty()) return;
   m->comms.resize(m->ids.size());
-  const Rccl& R = rccl();
+  const Rccl& R = m->R ? *m->R : rccl();
+  m->R = &R;
   const ncclResult_t r = R.comm_init_all(m->comms.data(), (int)m->ids.size(), m->ids.data());
   if (r != ncclSuccess) {
     m->comms.clear();
@@ -281,7 +309,7 @@ void Frame::gather() {
   uint64_t bytes = 0;
   if (m && m->rccl) {
     ensure_comms(m);
-    const Rccl& R = rccl();
+    const Rccl& R = *m->R;
     NCCLF(R.group_start());
     for (size_t i = 1; i < d.size(); ++i) {
       if (!d[i].count) continue;
@@ -359,8 +387,8 @@ mrt_ctx* multi_dev(const MultiDev* m, int i) { return m->devs[(size_t)i]; }
 void multi_free(MultiDev* m) {
   if (!m) return;
   delete m->scratch;
-  if (!m->comms.empty() && rccl().comm_destroy)
-    for (ncclComm_t c : m->comms) rccl().comm_destroy(c);
+  if (!m->comms.empty() && m->R && m->R->comm_destroy)
+    for (ncclComm_t c : m->comms) m->R->comm_destroy(c);
   for (mrt_ctx* c : m->devs) mrt_destroy(c);
   delete m;
 }
@@ -523,7 +551,6 @@ int mrt_create_multi(int n, const int* devices, mrt_ctx** out) {
 int mrt_debug_rccl_library(const char* name) {
   std::lock_guard<std::mutex> lk(g_rccl_mu);
   g_rccl_name = name && *name ? name : "librccl.so.1";
-  g_rccl_tried = false;
   return MRT_OK;
 }
 

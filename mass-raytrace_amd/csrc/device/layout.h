@@ -130,10 +130,21 @@ struct GpuMaterial {
   uint32_t pad1;
 };
 
+// RGBA8 texels (decoded c/255.0 exactly as texture.rs:44) in blocks of
+// 8 x 4 texels = 128 B, one L2 line (round 6): blocks row-major over the
+// texture, texels row-major inside a block, partial blocks zero-padded. A
+// bilinear tap (texture.rs:126-148) reads a 2x2 footprint, which row-major
+// rows spread over two lines always; in a block it stays in one line unless
+// it crosses a block edge (1.41 lines per tap on average).
+constexpr uint32_t kTexBlockW = 8, kTexBlockH = 4;
 struct GpuTexture {
   uint32_t width, height, wrap;
-  uint32_t offset;  // first texel in the texel array
+  uint32_t offset;  // first texel in the texel array (a multiple of 32: line-aligned)
 };
+// texel (x, y) of a texture whose rows hold tpr = ceil(width / 8) blocks
+MRT_HD uint32_t texel_index(uint32_t tpr, uint32_t x, uint32_t y) {
+  return (((y >> 2) * tpr + (x >> 3)) << 5) + ((y & 3u) << 3) + (x & 7u);
+}
 
 // Per-triangle shading record, 7 x float4 (112 B):
 //  0 {a.x a.y a.z b.x} 1 {b.y b.z c.x c.y} 2 {c.z na.x na.y na.z}

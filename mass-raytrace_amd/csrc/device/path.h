@@ -69,7 +69,8 @@ MRT_DEV float rust_fract(float x) { return x - truncf(x); }
 MRT_DEV uint32_t f2usize(float f) { return f > 0.0f ? (f < 4294967040.0f ? (uint32_t)f : 0xFFFFFFFFu) : 0u; }
 
 MRT_DEV V4 texel(const DevScene& S, const GpuTexture& t, uint32_t x, uint32_t y) {
-  uint32_t v = S.texels[MRT_IDX(S, t.offset + y * t.width + x, S.n_texels, 1)];
+  const uint32_t tpr = (t.width + kTexBlockW - 1) / kTexBlockW;  // layout.h: 8x4-texel blocks
+  uint32_t v = S.texels[MRT_IDX(S, t.offset + texel_index(tpr, x, y), S.n_texels, 1)];
   return V4{(float)(v & 255u) / 255.0f, (float)((v >> 8) & 255u) / 255.0f, (float)((v >> 16) & 255u) / 255.0f,
             (float)(v >> 24) / 255.0f};
 }
@@ -850,7 +851,11 @@ MRT_DEV void nf_finish(const TravIn& in, Trav& t, LocalCounters& lc) {
   const DevScene& S = in.S;
   bool ok = true;
   const float tau = fminf(t.t2, nf_cull(t.best));
+#ifdef MRT_PROBE_NF_NOCHECK  // measurement build only: the winner is not checked (NOT exact)
+  if (false) {
+#else
   if (t.prim != kRefNone) {
+#endif
     const uint32_t kind = t.prim >> 28, id = t.prim & 0x0FFFFFFFu;
     const uint32_t own = vnf_entry(S, kind == MRT_REF_SPHERE ? VNF_SPHERE : VNF_TRI, id, 0);
     if (t.hit_ret == kNoRet) {  // a world object (t.r is the world ray: every BLAS was left)
@@ -920,9 +925,13 @@ MRT_DEV void nf_node_test(const uint4& s0, const uint4& s1, const TRay& r, float
       const float t0 = vmax3(vmin1(lx, hx), vmin1(ly, hy), vmax1(vmin1(lz, hz), tmin));
       const float t1 = vmin3(vmax1(lx, hx), vmax1(ly, hy), vmin1(vmax1(lz, hz), tmax));
       const float m = fmaf(fabsf(t0) + fabsf(t1), 0x1p-19f, mabs);
-      hit[c] = !(t0 - t1 > m) || (s1.w & (kNfForceL << c));
+      const bool force = (s1.w & (kNfForceL << c)) != 0;
+      hit[c] = !(t0 - t1 > m) || force;
       ent[c] = t0;
-      ex[c] = fmaf(m, 2.0f, t1);  // every hit in the thickened box has t <= this (m covers t1's error and this rounding)
+      // every hit in the thickened box has t <= this (m covers t1's error and
+      // this rounding); a forced child holds a wild instance, whose hits the
+      // world margin does not place inside the box: no exit bound below it
+      ex[c] = force ? INFINITY : fmaf(m, 2.0f, t1);
     }
     return;
   }
@@ -958,7 +967,11 @@ MRT_DEV void trav_box_index_nf(const TravIn& in, const NfStack& k, Trav& t, Loca
   float e[2], x[2];
   // the hits this node must keep have t <= min(cull(best), nl)
   const float cb = nf_cull(t.best);
+#ifdef MRT_PROBE_NF_ZERO_RHO  // measurement build only: no rounding margin (NOT exact)
+  const float rho = 0.0f;
+#else
   const float rho = nf_rho_node(t.nfl, fminf(cb, t.nl));
+#endif
   nf_node_test(t.s0, t.s1, t.r, in.tmin, cb, rho, h, e, x);
   const uint32_t base = t.s1.w & kNfIdx, right = base + (t.s0.w >> 24);
   if (h[0] && h[1]) {

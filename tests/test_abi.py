@@ -106,7 +106,22 @@ def test_transport_choice_and_rccl_fallback():
     assert massrt.debug_transport([0, 0, 0]) == "peer"
     t = massrt.debug_transport([0, 1], rccl_library="librccl_missing_for_test.so")
     assert t.startswith("peer (RCCL unavailable: RCCL (librccl_missing_for_test.so) is not available"), t
-    # the real loader (ROCm's librccl is in this image): RCCL between distinct devices
-    assert massrt.debug_transport([0, 1, 2, 3, 4, 5, 6, 7]) == "rccl"
-    # the hook is reset: the next context opens the default library again
-    assert massrt.debug_transport([3, 5]) == "rccl"
+    # the real loader: RCCL between distinct devices where librccl opens (it
+    # is in this image); elsewhere the peer-copy fallback is the right answer
+    import ctypes
+
+    try:
+        ctypes.CDLL("librccl.so.1")
+        have_rccl = True
+    except OSError:
+        try:
+            ctypes.CDLL("/opt/rocm/lib/librccl.so.1")
+            have_rccl = True
+        except OSError:
+            have_rccl = False
+    t8 = massrt.debug_transport([0, 1, 2, 3, 4, 5, 6, 7])
+    t2 = massrt.debug_transport([3, 5])  # the hook is reset: the default library again
+    if have_rccl:
+        assert t8 == "rccl" and t2 == "rccl", (t8, t2)
+    else:
+        assert t8.startswith("peer (RCCL unavailable") and t2.startswith("peer (RCCL unavailable"), (t8, t2)

@@ -98,6 +98,47 @@ def test_alpha_mesh_through_model_and_instance(nf_ctx, variant):
     assert np.array_equal(g, ob)
 
 
+def test_wild_instances(nf_ctx, golden_dir):
+    """Instances whose rounding the world margin does not cover ("wild":
+    cond(fwd) x cond(inv) far above 2^-14 per unit, nf_tree.cpp wild()) are
+    never culled; the nodes on their path force the child and carry no exit
+    bound into the instance's BLAS (path.h nf_node_test). Thin
+    slabs scaled 1:3000, crossing each other, non-wild cubes and spheres, rays
+    from everywhere — and grazing the slabs — against the oracle."""
+    def scene(x):
+        x.background(massrt.BG_SKY)
+        lam = x.material(massrt.MAT_LAMBERTIAN, x.solid(0.6, 0.5, 0.4))
+        glow = x.material(massrt.MAT_DIFFUSE_LIGHT, 0, 0.0, (4.0, 4.0, 4.0))
+        cube = x.model_from_ply(golden_dir / "cube.ply", lam)
+        for k in range(6):  # wild: 12 x 0.004 x 9
+            x.add_instance(cube, (0.7 * k - 2.0, 0.3 * k - 0.6, -0.5 * k), (0.1 * k, 0.05, 0.02 * k), (12.0, 0.004, 9.0),
+                           glow if k % 2 else NO_MAT)
+        for k in range(5):  # ordinary
+            x.add_instance(cube, (1.1 * k - 2.0, 0.2, 1.0 - 0.4 * k), (0.0, 0.13 * k, 0.0), (0.4, 0.4, 0.4))
+        for k in range(4):
+            x.add_sphere(x.material(massrt.MAT_METAL, x.solid(0.8, 0.8, 0.8), 0.1), (k - 1.5, -0.2, 0.3 * k), 0.35)
+        x.build_bvh()
+        x.camera(45.0, (0.5, 1.5, 7), (0, 0, 0), aspect=ASPECT)
+
+    NO_MAT = massrt.NO_MATERIAL
+    b, o = build_both(scene)
+    nf_ctx.upload(b)
+    assert nf_ctx.tuning()["traversal"] == massrt.TRAVERSAL_NEAR_FIRST
+    r = np.random.default_rng(5)
+    o1 = r.uniform(-4, 4, (60_000, 3))
+    d1 = r.normal(size=(60_000, 3))
+    # grazing the slabs: nearly in the y = const plane of the slabs
+    o2 = np.concatenate([r.uniform(-6, 6, (60_000, 1)), r.uniform(-1, 1, (60_000, 1)), r.uniform(-6, 6, (60_000, 1))], 1)
+    d2 = np.concatenate([r.normal(size=(60_000, 1)), r.normal(size=(60_000, 1)) * 1e-3, r.normal(size=(60_000, 1))], 1)
+    rays = np.concatenate([np.concatenate([o1, d1], 1), np.concatenate([o2, d2], 1)]).astype(np.float32)
+    g, ob = nf_ctx.trace_rays(rays), o.trace_rays(rays)
+    assert (ob[:, 1] >> 28 != 0).sum() > 10_000
+    assert np.array_equal(g, ob), f"{int((g != ob).any(1).sum())} rays differ"
+    rgb, bo = nf_ctx.render(64, 36, 0, 2, seed=8)
+    orgb, obo = o.render(64, 36, 0, 2, seed=8)
+    assert np.array_equal(bo, obo) and rel_l2(rgb, orgb) <= RTOL
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_random_worlds_with_ties(nf_ctx, seed):
     """Coincident and touching primitives: equal t resolved to the later

@@ -275,9 +275,10 @@ void node_test(const uint32_t* a, const Ray& r, float tmin, float tmax, float nf
       const float t0 = fmaxf(fmaxf(fminf(tl[0], th[0]), fminf(tl[1], th[1])), fmaxf(fminf(tl[2], th[2]), tmin));
       const float t1 = fminf(fminf(fmaxf(tl[0], th[0]), fmaxf(tl[1], th[1])), fminf(fmaxf(tl[2], th[2]), tmax));
       const float m = std::fma(fabsf(t0) + fabsf(t1), 0x1p-19f, mabs);
-      hit[c] = !(t0 - t1 > m) || (a[7] & (kNfForceL << c));
+      const bool force = (a[7] & (kNfForceL << c)) != 0;
+      hit[c] = !(t0 - t1 > m) || force;
       ent[c] = t0;
-      ex[c] = std::fma(m, 2.0f, t1);
+      ex[c] = force ? INFINITY : std::fma(m, 2.0f, t1);  // a wild instance's hits: no exit bound
     } else {
       float mn[3], mx[3];
       for (int k = 0; k < 3; ++k) {
