@@ -75,6 +75,7 @@ sys.path.insert(0, str(REPO / "mass-raytrace_amd"))
 
 METRIC = "Msamples/sec (rays traced/sec) at 1920×1080×1024spp; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0
+N_CU, N_XCD = 256, 8  # MI355X: 256 CUs in 8 XCDs (MI355X_MICROARCH.md)
 # record stream bandwidth is cache-served: L2 aggregate with L1 reuse (MI355X_MICROARCH.md §L2)
 CACHE_PEAK_GBS = 36900.0
 
@@ -502,6 +503,40 @@ class RankRunner:
         self.ctx.close()
 
 
+def verify_gather(a, r, scene: str, devices, spp: int = 4) -> dict:
+    """N > 1, multi mode: outside the timed region, a
+    fresh image on the bench's own multi-device context renders `spp`
+    samples of the whole frame and gathers them onto device 0 over the
+    context's transport; a one-device context on devices[0] renders the same
+    (seed, samples). Each pixel is summed in sample order on one device, so
+    the two must be bit-identical."""
+    import numpy as np
+
+    import massrt
+
+    img = massrt.Image(r.ctx, r.W, r.H)
+    try:
+        img.render(a.seed, 0, spp, a.max_depth)
+        img.gather()
+        rgb, bounces, passes = img.read()
+    finally:
+        img.close()
+    one = massrt.Context(devices[0], options=context_options(a))
+    try:
+        b = massrt.Builder(1).builtin(scene, float(massrt.ASPECT_RATIO), str(asset_dir(scene)))
+        one.upload(b)
+        b.close()
+        orgb, ob = one.render(r.W, r.H, 0, spp, seed=a.seed, max_depth=a.max_depth)
+    finally:
+        one.close()
+    same_rgb = bool(np.array_equal(rgb.view(np.uint32), orgb.view(np.uint32)))
+    same_b = bool(np.array_equal(bounces, ob))
+    return {"identical": same_rgb and same_b and passes == spp, "rgb_bits_equal": same_rgb,
+            "bounces_equal": same_b, "spp": spp, "pixels": r.W * r.H,
+            "against": f"one-device context on device {devices[0]}, same seed and samples",
+            "differing_pixels": int((bounces != ob).sum() + (rgb != orgb).reshape(-1, 3).any(1).sum())}
+
+
 def timed_region(world, steps_fn, sync_fn, pg_dev=None):
     """Barrier + device sync on both sides of `steps_fn`; every rank's wall
     time, and the job's = the slowest rank's."""
@@ -593,6 +628,29 @@ def roofline_for(a, scene, cnt, ks, samples_total, elapsed, n_gpus, plan, trav: 
         # them back to the reference's walk (path.h nf_finish)
         "vnf_fallback_frac": round(cnt.get("vnf_fallbacks", 0) / max(cnt["segments"], 1), 6),
     }
+    # what a walk costs per unit of traversal work: frac
+    # prices algorithmic bytes, so a walk that needs fewer bytes reads lower
+    # at the same speed; CU time per segment and per box test rank walks by
+    # speed. From the HIP-event launch times (always) and, with a matching PMC
+    # profile, from its cycle counters (GRBM_GUI_ACTIVE over the 8 XCDs = the
+    # launch's clocks; TA_TA_BUSY_sum = address-unit cycles summed over CUs).
+    segs_per_launch = segs / trav_launches
+    visits_per_launch = cnt["node_visits"] / max(cnt["segments"], 1) * segs_per_launch
+    cu_ns = avg_ms * 1e6 * N_CU
+    roof["work_rate"] = {
+        "box_tests_per_segment": round(cnt["node_visits"] / max(cnt["segments"], 1), 2),
+        "cu_ns_per_segment": round(cu_ns / segs_per_launch, 2),
+        "cu_ns_per_box_test": round(cu_ns / max(visits_per_launch, 1), 3),
+        "basis": "HIP-event launch time x 256 CUs / (counted box tests or segments per launch); "
+                 "NF node records count as 2 box tests"}
+    kt = (pj or {}).get("kernels", {}).get("k_trace", {}) if pmc_basis == "this configuration" else {}
+    if kt.get("GRBM_GUI_ACTIVE_units") and kt.get("pmc_launches"):
+        clocks = kt["GRBM_GUI_ACTIVE_units"] / N_XCD  # per launch (pmc_summary.py averages per launch)
+        roof["work_rate"]["cu_cycles_per_box_test"] = round(clocks * N_CU / max(visits_per_launch, 1), 2)
+        roof["work_rate"]["cu_cycles_per_segment"] = round(clocks * N_CU / segs_per_launch, 1)
+        if kt.get("TA_TA_BUSY_sum"):
+            roof["work_rate"]["ta_cycles_per_box_test"] = round(kt["TA_TA_BUSY_sum"] / max(visits_per_launch, 1), 2)
+        roof["work_rate"]["pmc"] = "profiles/" + pmc_path.name
     shade = None
     if cnt.get("shaded") and ks["shade_launches"] > 0:
         # k_shade: HBM-streaming (path state in and out, shading data, texels): shade_bytes()
@@ -698,6 +756,12 @@ def run_scene(a, scene: str, steps: int, warmup: int, rank: int, world: int, dev
                              "ms_per_step": round(g_ms / steps, 3),
                              "device_render_ms_per_step": [round(x / steps, 3) for x in r.device_ms()],
                              "per_rank_ms_per_step": [round(e / steps * 1e3, 3) for e in per_rank]}
+            try:
+                out["gather"]["check"] = verify_gather(a, r, scene, devices)
+                out["gather"]["identical"] = out["gather"]["check"]["identical"]
+            except Exception as e:  # a failed check must not hide the timed number
+                out["gather"]["check"] = {"identical": None, "error": str(e)}
+                out["gather"]["identical"] = None
         else:
             out["gather"] = {"path": "one process per GPU: mrt_render_device + torch.distributed gather",
                              "transport": "RCCL (dist.gather over xGMI)" if a.dist_backend == "nccl" else

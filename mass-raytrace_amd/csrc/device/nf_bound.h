@@ -42,6 +42,11 @@ struct NfBound {
   float ao0, ao1;        // A_o = ao0 + ao1 |d_obj|
   float orad;            // a ball about the origin holding every instanced BLAS's boxes
   float kmax;            // a ray walks near first only while its generic kappa is at most this (<= kNfKappaMax)
+  // normal cones (round 6, nf_cone_rg below): the generic term per unit t is
+  // at most kc |d|^2 2^k / (|d . c| - |d| chi) over a node whose generic
+  // triangles' normals lie in the cone (c, chi) and whose |c| M <= 2^(k+6);
+  // 0: the scene's trees carry no cones (no generic triangles)
+  float kc;
 };
 
 // The walk is run only when the generic-triangle kappa stays at most
@@ -118,15 +123,61 @@ MRT_HD float nf_rho_at(const NfBound& B, const NfCoef& c, float t) {
 // for t <= cb (rho is monotone in t; the line drops the caps and takes the
 // spheres' slope at min(cb |d|, ls), beyond which no sphere hit lies), so a
 // node whose hits have t <= nl costs one fma and one min (nf_rho_node).
+// The slope is kept in two parts, ra = ra0 + rg: rg is the generic
+// triangles' term (gen |d|^2, gen = aw1 or ao1), which a node's normal cone
+// may lower (nf_cone_rg); kd, dl and s128 are the ray's constants for that.
 struct NfLine {
-  float rcb, ra, rb;
+  float rcb, ra0, rg, rb;
+  float kd;    // kc |d|^2 (rounded up)
+  float dl;    // |d| (rounded up)
+  float s128;  // 128 (d.x + d.y + d.z): the bias of the cone's stored components
 };
-MRT_HD NfLine nf_line(const NfBound& B, const NfCoef& c, float cb) {
+// the line of a space whose margin per unit L is a0 + gen |d| (world: aw0,
+// aw1; an instance's object space: ao0, ao1 — nf_coef_world / _object)
+MRT_HD NfLine nf_line(const NfBound& B, const NfCoef& c, float cb, float a0, float gen, float d2, V3 d) {
   const float k = fmaf(B.s51, fminf(c.dl * cb, c.ls) + c.delta, B.s130);  // the spheres' slope per unit L
   constexpr float up = 1.0f + 0x1p-16f;
-  return NfLine{nf_rho_at(B, c, cb), fmaf(k, c.dl, c.a) * up, fmaf(k, c.delta, c.b) * up};
+  return NfLine{nf_rho_at(B, c, cb), fmaf(k, c.dl, a0 * c.dl) * up, (gen * c.dl) * c.dl * up,
+                fmaf(k, c.delta, c.b) * up, B.kc * d2 * up, c.dl, 128.0f * ((d.x + d.y) + d.z)};
 }
 // (a nearer cull bound cb' < cb keeps the line and caps it at nf_rho_node(l, cb'))
-MRT_HD float nf_rho_node(const NfLine& l, float t) { return fminf(l.rcb, fmaf(l.ra, t, l.rb)); }
+MRT_HD float nf_rho_node(const NfLine& l, float t) { return fminf(l.rcb, fmaf(l.ra0 + l.rg, t, l.rb)); }
+
+// ---- normal cones (round 6; DESIGN.md §4 "Normal cones") ----
+// The generic-triangle term comes from Moller-Trumbore's cancellation, which
+// the reference bounds only by its absolute |det| >= 1e-6 test (geom.rs:511):
+// priced that way, every ray pays for the worst direction and rho grows to
+// ~3e-3 L for camera rays of the 1M-triangle mesh. But det = -d . N (N = ab x
+// ac), so over a node whose triangles' normals lie in a cone about an integer
+// vector c (|c| n_i within chord delta of c, each n_i up to sign):
+//   |det_i| >= |ab_i||ac_i| (|d . c| - |d| chi) / (|c| m_i),  m_i = |ab||ac|/|N|
+// where chi = |c| delta + 7.3u |c| M (the computed det's own error, M =
+// max m_i) + 3000u (this evaluation's rounding) — so the term
+// 24u |d| |ab||ac| / |det| <= 24u |c| M |d| / (|d . c| - |d| chi), and per
+// unit t the node's generic slope is at most kd 2^k / (|d . c| - |d| chi)
+// with |c| M <= 2^(k+6) (kc = 24.01u / (1 - kNfKappaMax), rounded up with the
+// slack of rcp, ldexp and these roundings). Where the cone says nothing
+// (a ray within the cone's grazing band: G <= 0) the node keeps rg.
+// The node record carries c + 128 in the low byte of each origin word (an
+// origin is any float at or below the children's minimum: nf_tree.cpp picks
+// one with that byte) and, in bits 25-31 of slot0.w, j (chi = 2^(j - 3);
+// j = 15: no cone) and k.
+constexpr uint32_t kNfConeNone = 15u;  // j of a node without a cone (chi = 2^12 > any |c|)
+MRT_HD float nf_cone_rg(const NfLine& l, uint32_t ox, uint32_t oy, uint32_t oz, uint32_t w, V3 d) {
+  const float cx = (float)(ox & 0xFFu), cy = (float)(oy & 0xFFu), cz = (float)(oz & 0xFFu);  // c + 128
+  const float dc = fabsf(fmaf(d.z, cz, fmaf(d.y, cy, fmaf(d.x, cx, -l.s128))));
+  const uint32_t code = w >> 25;
+  const float G = fmaf(-l.dl, ldexpf(1.0f, (int)(code & 15u) - 3), dc);
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float rcp = __builtin_amdgcn_rcpf(fmaxf(G, 0x1p-100f));  // within an ulp: kc's slack
+#else
+  const float rcp = 1.0f / fmaxf(G, 0x1p-100f);
+#endif
+  return fminf(l.rg, ldexpf(l.kd, (int)(code >> 4)) * rcp);
+}
+// rho of a node (record words o.x, o.y, o.z, w) for hits at t or before
+MRT_HD float nf_rho_cone(const NfLine& l, float t, uint32_t ox, uint32_t oy, uint32_t oz, uint32_t w, V3 d) {
+  return fminf(l.rcb, fmaf(l.ra0 + nf_cone_rg(l, ox, oy, oz, w, d), t, l.rb));
+}
 
 }  // namespace mrt

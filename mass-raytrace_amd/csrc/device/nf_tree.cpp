@@ -157,6 +157,11 @@ struct Node {
   int32_t l = -1, r = -1;
   uint32_t first = 0, count = 0, axis = 0;
   uint32_t force = 0;  // kNfForceL / kNfForceR: that child is never culled (wild instances)
+  uint32_t lo = 0, hi = 0;  // the subtree's items [lo, hi) (build partitions them in place)
+  // normal cone of the subtree's generic triangles (nf_bound.h nf_cone_rg):
+  // c + 128 per axis, and the code {j (4 bits), k (3 bits)}
+  uint8_t cb[3] = {128, 128, 128};
+  uint8_t code = kNfConeNone | 7u << 4;
 };
 struct Tree {
   std::vector<Node> nodes;
@@ -180,6 +185,7 @@ struct Tree {
       cb.grow(c[0], c[1], c[2]);
     }
     const int32_t id = (int32_t)nodes.size();
+    n.lo = b, n.hi = e;
     nodes.push_back(n);
     const uint32_t cnt = e - b;
     constexpr uint32_t kLeaf = 4;
@@ -282,13 +288,25 @@ struct Builder {
   // 254 steps covering the union (one step of slack for the rounding of the
   // double arithmetic below, whose error is < 2^-40 of a step); planes rounded
   // outward. false: a box is not finite (or past the exponent range).
-  static bool quantize(const Box& a, const Box& b, uint32_t o[3], uint32_t& ew, uint32_t q[3]) {
+  // The origin of axis k is the largest float at or below the children's
+  // minimum whose low mantissa byte is cb[k] (the node's cone component,
+  // nf_bound.h): the planes are quantized from that exact float, so the byte
+  // costs at most 2^-15 of |origin| of range, never tightness.
+  static float origin_with_byte(float v, uint8_t byte) {
+    if (!(fabsf(v) >= 0x1p-100f)) v = fminf(v, -0x1p-100f);  // zero or tiny: a normal origin below it
+    uint32_t u = f2u(v), c = (u & ~0xFFu) | byte;
+    if (u2f(c) > v) c = v > 0.0f ? c - 0x100u : c + 0x100u;  // one step of 256 ulps further down
+    return u2f(c);
+  }
+  static bool quantize(const Box& a, const Box& b, const uint8_t cb[3], uint32_t o[3], uint32_t& ew, uint32_t q[3]) {
     uint8_t bytes[12];
     ew = 0;
     for (int k = 0; k < 3; ++k) {
-      const float org = fminf(a.mn[k], b.mn[k]);
+      const float mn = fminf(a.mn[k], b.mn[k]);
       const double hi = std::max((double)a.mx[k], (double)b.mx[k]);
-      if (!(fabsf(org) < INFINITY) || !(fabs(hi) < INFINITY)) return false;
+      if (!(fabsf(mn) < INFINITY) || !(fabs(hi) < INFINITY)) return false;
+      const float org = origin_with_byte(mn, cb[k]);
+      if (!(fabsf(org) < INFINITY) || !(org <= mn) || (f2u(org) & 0xFFu) != cb[k]) return false;
       const double ext = hi - (double)org;
       int e = kNfExpMin;
       while (std::ldexp(254.0, e) < ext) ++e;
@@ -338,9 +356,10 @@ struct Builder {
     const uint32_t lsz = child_slots(t, L), rsz = child_slots(t, R), base = n_slots();
     for (uint32_t z = 0; z < 4 * (lsz + rsz); ++z) w.push_back(0);
     uint32_t o[3], ew, q[3];
-    if (!quantize(L.b, R.b, o, ew, q)) return false;
+    if (!quantize(L.b, R.b, n.cb, o, ew, q)) return false;
+    if (lsz < 2 || lsz > 3) return false;  // a node (2 slots) or a leaf's first record (2 or 3)
     uint32_t* rec = &w[4 * (size_t)at];
-    rec[0] = o[0], rec[1] = o[1], rec[2] = o[2], rec[3] = ew | lsz << 24;
+    rec[0] = o[0], rec[1] = o[1], rec[2] = o[2], rec[3] = ew | (lsz - 2) << 24 | (uint32_t)n.code << 25;
     rec[4] = q[0], rec[5] = q[1], rec[6] = q[2], rec[7] = kBoxFlag | n.force | base;
     s.nf_boxes++;
     for (const auto& [c, pos] : {std::pair<const Node*, uint32_t>{&L, base}, {&R, base + lsz}}) {
@@ -557,6 +576,106 @@ struct Builder {
     for (int k = 0; k < 3; ++k) p[k] = b.mn[k], p[3 + k] = b.mx[k];
   }
 
+  // Normal cones of every internal node of tree t (nf_bound.h nf_cone_rg):
+  // over the node's generic triangles, an integer axis c (components within
+  // +-127, stored as c + 128) near the mean of their normals (each up to
+  // sign), the chord chi of the widest normal from it (in |c| units, plus the
+  // computed determinant's error and the evaluation's rounding), and the
+  // exponent k with |c| M <= 2^(k+6). A node holding an instance or model
+  // whose BLAS has generic triangles (their world-space rounding is the
+  // instance term, not a cone's) or a cone wider than a hemisphere's chord
+  // gets none: the node keeps the ray's generic term.
+  void fit_cones(Tree& t) {
+    struct N {
+      double n[3], m;
+      int kind;  // 0 none, 1 generic triangle, 2 poison (generic instance / model)
+    };
+    std::vector<N> it(t.items.size());
+    for (size_t i = 0; i < t.items.size(); ++i) {
+      const uint32_t r = t.items[i].rec;
+      N& x = it[i];
+      x.kind = 0;
+      const uint32_t kd = kind_of(w, r);
+      if (kd == KIND_TRI) {
+        const float ab[3] = {u2f(w[4 * (size_t)r + 3]), u2f(w[4 * (size_t)r + 4]), u2f(w[4 * (size_t)r + 5])};
+        const float ac[3] = {u2f(w[4 * (size_t)r + 8]), u2f(w[4 * (size_t)r + 9]), u2f(w[4 * (size_t)r + 10])};
+        if (!(tri_bound(ab, ac).a1 > 0)) continue;
+        // N = ab x ac: each product of two floats exact in double, one rounding per component
+        const double nn[3] = {(double)ab[1] * ac[2] - (double)ab[2] * ac[1], (double)ab[2] * ac[0] - (double)ab[0] * ac[2],
+                              (double)ab[0] * ac[1] - (double)ab[1] * ac[0]};
+        const double ln = norm3(nn);
+        const double dab[3] = {ab[0], ab[1], ab[2]}, dac[3] = {ac[0], ac[1], ac[2]};
+        x.kind = 2;  // a degenerate generic triangle: no cone can bound it
+        if (!(ln > 0) || !(ln < INFINITY)) continue;
+        x.kind = 1;
+        for (int k = 0; k < 3; ++k) x.n[k] = nn[k] / ln;
+        x.m = norm3(dab) * norm3(dac) / ln * (1.0 + 1e-9);
+      } else if (kd == KIND_INST || kd == KIND_MODEL) {
+        auto rg = region_of.find(w[4 * (size_t)r + 1]);
+        if (rg != region_of.end() && blas_bound[rg->second].a1 > 0) x.kind = 2;
+      }
+    }
+    const double u = kU;
+    for (Node& nd : t.nodes) {
+      if (nd.l < 0) continue;
+      nd.cb[0] = nd.cb[1] = nd.cb[2] = 128;
+      nd.code = (uint8_t)(kNfConeNone | 7u << 4);
+      bool poison = false, any = false;
+      double ax[3] = {0, 0, 0};
+      for (uint32_t i = nd.lo; i < nd.hi && !poison; ++i) {
+        if (it[i].kind == 2) poison = true;
+        if (it[i].kind != 1) continue;
+        if (!any) ax[0] = it[i].n[0], ax[1] = it[i].n[1], ax[2] = it[i].n[2], any = true;
+      }
+      if (poison) continue;
+      if (!any) {  // no generic triangle below: any cone is valid; the narrowest slope is k = 0
+        nd.cb[0] = 255, nd.code = 0;  // c = (127, 0, 0), chi = 1/8
+        continue;
+      }
+      for (int pass = 0; pass < 2; ++pass) {  // the mean of the normals aligned to the current axis
+        double sm[3] = {0, 0, 0};
+        for (uint32_t i = nd.lo; i < nd.hi; ++i) {
+          if (it[i].kind != 1) continue;
+          const double* n = it[i].n;
+          const double sg = n[0] * ax[0] + n[1] * ax[1] + n[2] * ax[2] < 0 ? -1.0 : 1.0;
+          for (int k = 0; k < 3; ++k) sm[k] += sg * n[k];
+        }
+        const double l = norm3(sm);
+        if (!(l > 0)) break;
+        for (int k = 0; k < 3; ++k) ax[k] = sm[k] / l;
+      }
+      const double mx = std::max(std::fabs(ax[0]), std::max(std::fabs(ax[1]), std::fabs(ax[2])));
+      if (!(mx > 0)) continue;
+      int c[3];
+      for (int k = 0; k < 3; ++k) c[k] = (int)std::lround(127.0 * ax[k] / mx);
+      const double dc[3] = {(double)c[0], (double)c[1], (double)c[2]};
+      const double lc = norm3(dc);
+      double chord = 0, M = 0;
+      for (uint32_t i = nd.lo; i < nd.hi; ++i) {
+        if (it[i].kind != 1) continue;
+        const double* n = it[i].n;
+        double dm = 0, dp = 0;
+        for (int k = 0; k < 3; ++k) {
+          const double q = dc[k] / lc;
+          dm += (n[k] - q) * (n[k] - q), dp += (n[k] + q) * (n[k] + q);
+        }
+        chord = std::max(chord, std::sqrt(std::min(dm, dp)));
+        M = std::max(M, it[i].m);
+      }
+      if (!(chord < 1.0)) continue;  // wider than 60 degrees: the grazing band is most of the sphere
+      const double chi = lc * chord * (1.0 + 1e-9) + 7.3 * u * lc * M + 3000.0 * u;
+      int j = 3 + (int)std::ceil(std::log2(chi));
+      while (std::ldexp(1.0, j - 3) < chi) ++j;
+      j = std::max(j, 0);
+      int kk = std::max(0, (int)std::ceil(std::log2(lc * M)) - 6);
+      while (std::ldexp(1.0, kk + 6) < lc * M) ++kk;
+      if (j >= (int)kNfConeNone || kk > 7) continue;
+      for (int k = 0; k < 3; ++k) nd.cb[k] = (uint8_t)(c[k] + 128);
+      nd.code = (uint8_t)(j | kk << 4);
+      s.nf_cones++;
+    }
+  }
+
   // the per-scene rule's verdict before building (render.hip apply_options):
   // the reference walk for a generic-triangle term or a big instanced world
   bool auto_declines() const {
@@ -684,6 +803,13 @@ struct Builder {
     world.max_depth = kNfStack - (has_blas ? 2 + blas_depth : 0);
     world.build(0, (uint32_t)world.items.size(), 0);
     if (!wild_items.empty()) world.mark_forced(0);
+    if (aw1 > 0 || ao1 > 0)  // generic triangles somewhere: every tree's nodes get their cones
+      for (Tree* t : [&] {
+             std::vector<Tree*> v{&world};
+             for (Tree& b : blas) v.push_back(&b);
+             return v;
+           }())
+        fit_cones(*t);
     s.nf_stack_need = world.depth + (has_blas ? 2 + blas_depth : 0);
     if (s.nf_stack_need > kNfStack) return (s.nf_note = "trees deeper than the walk's stack", true);
     // the constants (rounded up) of nf_bound.h
@@ -711,6 +837,11 @@ struct Builder {
     B.kw1 = f_up(world_tri.k1), B.ko1 = f_up(ko1);
     B.ao0 = f_up(ao0), B.ao1 = f_up(ao1), B.orad = f_up(orad);
     B.kmax = kNfKappaMax;
+    // the cones' slope constant (nf_bound.h nf_cone_rg): 1.0001 * 24u * 2^6 /
+    // (1 - kappa max), with 2^-17 for rcp (an ulp), the kd product and d2's
+    // roundings, and G's
+    B.kc = (aw1 > 0 || ao1 > 0) ? f_up(1.0001 * 24.0 * kU * 64.0 / (1.0 - 1.01 * (double)kNfKappaMax) * (1.0 + 0x1p-17))
+                                : 0.0f;
     if (r_max > 0) {
       ball(sph_box, B.sc, B.sr);
       B.s51 = f_up(51.2 * kU / r_min), B.s28 = f_up(27.8 * kU), B.s130 = f_up(130.2 * kU), B.s11 = f_up(11.2 * kU * r_max);
@@ -746,6 +877,7 @@ bool build_nf_trees(const mrt_scene_desc& d, HostScene& s, std::string& err) {
     s.slots.resize(keep);
     s.nf_boxes = 0;
     s.nf_wild = 0;
+    s.nf_cones = 0;
     s.vnf_leaf.clear();
   }
   return ok;

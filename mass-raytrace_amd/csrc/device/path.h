@@ -753,8 +753,9 @@ MRT_DEV float nf_cull(float best) { return fmaf(fabsf(best), 0x1p-10f, best); }
 // far a node's boxes are thickened (trav_box_index_nf)
 MRT_DEV void nf_margin(const TravIn& in, Trav& t) {
   const bool obj = t.ret != kNoRet && (t.ret & kRetInstance);
-  const NfCoef c = obj ? nf_coef_object(in.S.nfb, t.r.o, t.r.a.b) : nf_coef_world(in.S.nfb, t.r.o, t.r.a.b);
-  t.nfl = nf_line(in.S.nfb, c, nf_cull(t.best));
+  const NfBound& B = in.S.nfb;
+  const NfCoef c = obj ? nf_coef_object(B, t.r.o, t.r.a.b) : nf_coef_world(B, t.r.o, t.r.a.b);
+  t.nfl = nf_line(B, c, nf_cull(t.best), obj ? B.ao0 : B.aw0, obj ? B.ao1 : B.aw1, t.r.a.b, t.r.d);
 }
 // the walk starts at the NF world tree (trav_init): rays its bound does not
 // cover take the reference's walk instead
@@ -970,10 +971,13 @@ MRT_DEV void trav_box_index_nf(const TravIn& in, const NfStack& k, Trav& t, Loca
 #ifdef MRT_PROBE_NF_ZERO_RHO  // measurement build only: no rounding margin (NOT exact)
   const float rho = 0.0f;
 #else
-  const float rho = nf_rho_node(t.nfl, fminf(cb, t.nl));
+  // the node's normal cone narrows the generic-triangle term (nf_bound.h
+  // nf_cone_rg); scenes without generic triangles (kc == 0) skip it
+  const float rho = in.S.nfb.kc > 0.0f ? nf_rho_cone(t.nfl, fminf(cb, t.nl), t.s0.x, t.s0.y, t.s0.z, t.s0.w, t.r.d)
+                                       : nf_rho_node(t.nfl, fminf(cb, t.nl));
 #endif
   nf_node_test(t.s0, t.s1, t.r, in.tmin, cb, rho, h, e, x);
-  const uint32_t base = t.s1.w & kNfIdx, right = base + (t.s0.w >> 24);
+  const uint32_t base = t.s1.w & kNfIdx, right = base + 2u + ((t.s0.w >> 24) & 1u);  // lsz - 2 in bit 24 (layout.h)
   if (h[0] && h[1]) {
     const bool lfirst = !(e[1] < e[0]);
     nf_push(k, t, lfirst ? right : base);

@@ -57,6 +57,7 @@ struct HostScene {
   std::string nf_note;  // why a scene has no NF trees
   NfBound nfb{};         // the walk's rounding margins (nf_bound.h, nf_tree.cpp)
   uint32_t nf_wild = 0;  // instances the world margin does not cover: never culled
+  uint32_t nf_cones = 0;  // NF nodes carrying a normal cone (nf_bound.h nf_cone_rg)
   // tools/slab_check: set before building to keep every leaf object's NF box
   // (6 floats per vnf_leaf slot: mn xyz, mx xyz) and which instances are wild
   bool keep_nf_boxes = false;

@@ -73,6 +73,27 @@ def test_near_first_walk_mesh_and_menger(slab_check, assets_dir, scene):
     assert r.returncode == 0 and " nf: 0 of 20000 rays differ" in r.stdout, r.stdout + r.stderr
     checks, worst, over, line = _bound(r.stdout)
     assert over == 0 and worst < 0.25, line
+    if scene == "mesh_ply":  # normal cones (nf_bound.h nf_cone_rg): the generic term priced per node
+        cones = [x for x in r.stdout.splitlines() if " nf cones: " in x][0]
+        assert int(cones.split("nf cones: ")[1].split(" of")[0]) > 100_000, cones
+        per_ray = float(r.stdout.split(" box tests ")[1].split(" vs")[0])
+        assert per_ray < 50.0, r.stdout  # 64.6 with the worst-case |det| >= 1e-6 pricing, 41.2 with no margin
+
+
+@pytest.mark.slow
+def test_near_first_grazing_rays_mesh_cones(slab_check, assets_dir):
+    """The 1M-triangle mesh's generic triangles under the normal-cone bound
+    (round 6): rays within 10^-8..10^-1.5 rad of a triangle's plane sit in
+    the cone's grazing band, where each node falls back to the worst-case
+    |det| >= 1e-6 term; every accepted hit still lies within the (cone-
+    narrowed) rho of every NF node above it, and no closest hit differs."""
+    r = subprocess.run([str(slab_check), "mesh_ply", "20000", str(assets_dir), "graze"], capture_output=True,
+                       text=True, timeout=900)
+    line = [x for x in r.stdout.splitlines() if " nf: " in x][0]
+    assert " nf: 0 of 20000 rays differ" in line, line
+    checks, worst, over, bline = _bound(r.stdout)
+    assert checks > 20000 and over == 0 and worst < 0.25, bline
+    assert r.returncode == 0, r.stdout + r.stderr
 
 
 @pytest.mark.parametrize("scene", ["cornell", "cube_field", "sphere_grid"])

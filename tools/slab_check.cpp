@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <random>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../mass-raytrace_amd/csrc/device/upload.h"
@@ -135,18 +136,85 @@ struct BoundCheck {
   double worst = 0, worst_cap = 0;  // max dist / rho, max L / L_cap
 };
 BoundCheck* g_bc = nullptr;
+
+// NF tree parents (normal cones, round 6): every node a primitive's test
+// passes through on the near-first walk thickens its boxes by that node's
+// rho, so each must cover the hit: leaf_parent[vnf slot] is the NF node
+// holding the primitive's leaf, nf_parent the node above a node (~0: a root)
+std::unordered_map<uint32_t, uint32_t> g_nf_parent;
+std::vector<uint32_t> g_leaf_parent;
+uint32_t nf_vslot(const HostScene& s, const uint32_t* a) {
+  switch (a[7]) {
+    case KIND_TRI: return s.vnf_base[VNF_TRI] + (a[6] & kTriIdMask);
+    case KIND_SPHERE: return s.vnf_base[VNF_SPHERE] + a[4];
+    case KIND_INST: return s.vnf_base[VNF_INST] + a[0];
+    default: return s.vnf_base[VNF_MODEL] + a[0];
+  }
+}
+void map_nf_tree(const HostScene& s, uint32_t root, std::vector<uint8_t>& seen_blas) {
+  const uint32_t* w = s.slots.data();
+  std::vector<std::pair<uint32_t, uint32_t>> st{{root, ~0u}};
+  while (!st.empty()) {
+    const auto [i, par] = st.back();
+    st.pop_back();
+    const uint32_t* a = w + 4 * (size_t)i;
+    if (a[7] & kBoxFlag) {
+      g_nf_parent[i] = par;
+      const uint32_t base = a[7] & kNfIdx;
+      st.push_back({base, i});
+      st.push_back({base + 2 + ((a[3] >> 24) & 1u), i});
+      continue;
+    }
+    for (uint32_t r = i;;) {
+      const uint32_t* b = w + 4 * (size_t)r;
+      g_leaf_parent[nf_vslot(s, b)] = par;
+      uint32_t next;
+      if (b[7] == KIND_TRI) {
+        next = b[11];
+      } else if (b[7] == KIND_SPHERE) {
+        next = b[5];
+      } else {
+        if (!seen_blas[b[1]]) {
+          seen_blas[b[1]] = 1;
+          map_nf_tree(s, b[1], seen_blas);
+        }
+        next = b[2];
+      }
+      if (next == kNfPop) break;
+      r = next;
+    }
+  }
+}
+// the smallest rho over the NF nodes a hit's primitive (vnf slot) sits below,
+// each with its normal cone (path.h trav_box_index_nf), at the hit's t
+float cone_rho_min(const HostScene& s, uint32_t vslot, V o, V d, float t, bool obj) {
+  const mrt::V3 oo{o.x, o.y, o.z}, dd{d.x, d.y, d.z};
+  const float d2 = (d.x * d.x + d.y * d.y) + d.z * d.z;
+  const NfBound& B = s.nfb;
+  const NfCoef c = obj ? nf_coef_object(B, oo, d2) : nf_coef_world(B, oo, d2);
+  const NfLine l = nf_line(B, c, t, obj ? B.ao0 : B.aw0, obj ? B.ao1 : B.aw1, d2, dd);
+  float rho = nf_rho_at(B, c, t);
+  if (!(B.kc > 0) || vslot >= g_leaf_parent.size()) return rho;
+  const uint32_t* w = s.slots.data();
+  for (uint32_t n = g_leaf_parent[vslot]; n != ~0u; n = g_nf_parent[n]) {
+    const uint32_t* a = w + 4 * (size_t)n;
+    rho = std::min(rho, nf_rho_cone(l, t, a[0], a[1], a[2], a[3], dd));
+  }
+  return rho;
+}
 double box_dist(const float* b, double x, double y, double z) {
   const double p[3] = {x, y, z};
   double m = 0;
   for (int k = 0; k < 3; ++k) m = std::max(m, std::max((double)b[k] - p[k], p[k] - (double)b[3 + k]));
   return m;
 }
-void check_hit(const HostScene& s, const float* box, V o, V d, float t, bool obj) {
+void check_hit(const HostScene& s, const float* box, V o, V d, float t, bool obj, uint32_t vslot = ~0u) {
   if (!box || std::isnan(box[0])) return;
   const double x = (double)o.x + (double)t * d.x, y = (double)o.y + (double)t * d.y, z = (double)o.z + (double)t * d.z;
   const mrt::V3 oo{o.x, o.y, o.z};
   const NfCoef c = obj ? nf_coef_object(s.nfb, oo, dot(d, d)) : nf_coef_world(s.nfb, oo, dot(d, d));
-  const float rho = nf_rho_at(s.nfb, c, t);
+  // the rho of every NF node above the primitive, narrowed by its cone
+  const float rho = vslot == ~0u ? nf_rho_at(s.nfb, c, t) : cone_rho_min(s, vslot, o, d, t, obj);
   const float cap = nf_rho_at(s.nfb, c, INFINITY);
   const double dist = box_dist(box, x, y, z);
 
@@ -211,7 +279,7 @@ Result walk_plain(const HostScene& s, V o, V d, Stats* st = nullptr) {
       if (g_bc && tri_hit({f(a[0]), f(a[1]), f(a[2])}, {f(a[3]), f(a[4]), f(a[5])}, {f(a[8]), f(a[9]), f(a[10])}, r.o,
                           r.d, kTmin, INFINITY, t)) {
         const bool inst = ret != ~0u && (ret & 0x80000000u);
-        check_hit(s, leaf_box(s, VNF_TRI, a[6] & kTriIdMask), r.o, r.d, t, inst);
+        check_hit(s, leaf_box(s, VNF_TRI, a[6] & kTriIdMask), r.o, r.d, t, inst, s.vnf_base[VNF_TRI] + (a[6] & kTriIdMask));
         if (inst) {  // the same hit in world space against the instance's world box
           const uint32_t cid = w[4 * (size_t)((ret & 0x7FFFFFFFu) - 2)];
           if (s.nf_inst_wild.empty() || !s.nf_inst_wild[cid]) check_hit(s, leaf_box(s, VNF_INST, cid), wr.o, wr.d, t, false);
@@ -326,7 +394,8 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks, uin
     const bool obj = ret != ~0u && (ret & 0x80000000u);
     const mrt::V3 oo{r.o.x, r.o.y, r.o.z};
     nfc = obj ? nf_coef_object(s.nfb, oo, dot(r.d, r.d)) : nf_coef_world(s.nfb, oo, dot(r.d, r.d));
-    nfl = nf_line(s.nfb, nfc, cull());
+    nfl = nf_line(s.nfb, nfc, cull(), obj ? s.nfb.ao0 : s.nfb.aw0, obj ? s.nfb.ao1 : s.nfb.aw1, dot(r.d, r.d),
+                  mrt::V3{r.d.x, r.d.y, r.d.z});
   };
   margin();
   auto pop = [&]() {
@@ -371,8 +440,11 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks, uin
       if (st) st->boxes += 2, st->loads += 2;
       bool h[2];
       float e[2], x[2];
-      node_test(a, r, kTmin, cull(), nf_rho_node(nfl, fminf(cull(), nl)), h, e, x);
-      const uint32_t base = k & kNfIdx, right = base + (a[3] >> 24);
+      const float tn = fminf(cull(), nl);
+      const float rho = s.nfb.kc > 0 ? nf_rho_cone(nfl, tn, a[0], a[1], a[2], a[3], mrt::V3{r.d.x, r.d.y, r.d.z})
+                                     : nf_rho_node(nfl, tn);
+      node_test(a, r, kTmin, cull(), getenv("SLAB_NO_CONE") ? nf_rho_node(nfl, tn) : rho, h, e, x);
+      const uint32_t base = k & kNfIdx, right = base + 2 + ((a[3] >> 24) & 1u);
       if (h[0] && h[1]) {
         const bool lf = !(e[1] < e[0]);
         stack.push_back(lf ? right : base);
@@ -531,6 +603,12 @@ int main(int argc, char** argv) {
   if (nf && !s.nf_ok) {
     printf("%-14s nf: no near-first trees (%s)\n", argv[1], s.nf_note.c_str());
     return 0;
+  }
+  if (nf && s.nf_ok) {  // NF parents for the cone-narrowed bound checks
+    g_leaf_parent.assign(s.vnf_leaf.size() / 2, ~0u);
+    std::vector<uint8_t> seen(s.slots.size() / 4, 0);
+    map_nf_tree(s, s.nf_world, seen);
+    printf("%-14s nf cones: %u of %u nodes carry one, kc %.3g\n", argv[1], s.nf_cones, s.nf_boxes, (double)s.nfb.kc);
   }
   uint64_t nf_bad = 0, nf_fallbacks = 0, nf_starts_ref = 0, nf_even = 0, nf_odd = 0;
   BoundCheck bc;
