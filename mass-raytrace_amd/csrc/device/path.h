@@ -970,6 +970,8 @@ MRT_DEV void trav_box_index_nf(const TravIn& in, const NfStack& k, Trav& t, Loca
   const float cb = nf_cull(t.best);
 #ifdef MRT_PROBE_NF_ZERO_RHO  // measurement build only: no rounding margin (NOT exact)
   const float rho = 0.0f;
+#elif defined(MRT_PROBE_NF_NOCONE)  // measurement build only: the ray's generic term everywhere (exact, looser)
+  const float rho = nf_rho_node(t.nfl, fminf(cb, t.nl));
 #else
   // the node's normal cone narrows the generic-triangle term (nf_bound.h
   // nf_cone_rg); scenes without generic triangles (kc == 0) skip it
