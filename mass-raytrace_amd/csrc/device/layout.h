@@ -81,12 +81,14 @@ constexpr uint32_t kTriIdMask = 0x0FFFFFFFu;
 //           record or kNfPop (continue with the stack)
 //   INST / MODEL {id, nf_blas_root, next, 0} {0,0,0,INST|MODEL}
 constexpr uint32_t kNfIdx = 0x0FFFFFFFu;  // index bits of an NF node's children base
-// an NF node's slot1.w: its left / right child is never culled (the subtree
-// of "wild" instances, whose rounding the world margin does not cover; nf_tree.cpp)
+// an NF node's slot1.w: its left / right child's subtree holds a "wild"
+// instance, whose rounding the world margin does not cover (nf_tree.cpp): the
+// node's boxes are thickened by the wild margin too (nf_bound.h nf_rho_wild)
 constexpr uint32_t kNfForceL = 0x10000000u, kNfForceR = 0x20000000u;
 constexpr uint32_t kNfPop = 0x0FFFFFFFu;  // "next" of a leaf's last record: pop the stack
 constexpr int kNfExpMin = -100;            // smallest plane step 2^e (products with 1/d stay normal)
 constexpr uint32_t kNfStack = 24u;         // stack entries per lane (LDS): the trees' depth is capped to fit
+constexpr uint32_t kNfWildFew = 16u;       // a world of at most this many instances may leave big absolute terms out of its margin (nf_tree.cpp)
 constexpr uint32_t kNoParent = 0xFFFFFFFFu;
 // Verification record of a leaf object (DevScene::vnf_leaf[vnf_base[kind] + id]):
 //   {reference parent box record (kNoParent: a root object), order key}

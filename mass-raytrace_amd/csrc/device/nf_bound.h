@@ -180,4 +180,67 @@ MRT_HD float nf_rho_cone(const NfLine& l, float t, uint32_t ox, uint32_t oy, uin
   return fminf(l.rcb, fmaf(l.ra0 + nf_cone_rg(l, ox, oy, oz, w, d), t, l.rb));
 }
 
+// ---- wild instances (round 6; DESIGN.md §4 "Wild instances") ----
+// An instance whose rounding terms would dominate the world margin — a thin
+// light box (cond = |F||G| ~ 1.4e4: A ~ 0.047 per unit L), a 1000x floor (an
+// absolute term ~4e-4) — or any instance of a world with few of them
+// (kNfWildFew) stays out of the world margin (aw*, bw*). The nodes above it
+// never cull it (kNfForceL/R); its leaf record points at a WILD entry (layout.h)
+// holding its world box and its own instance term (nf_tree.cpp inst_term, the
+// bound of every instance): its hits lie within
+//   rho_x(t) = A min(|d| t, 2.5 (|o - c| + r + b)) + b,  A = a0 + a1 |d|,  b = b0 + b1 |o|
+// of that box ((c, r): a ball holding the box; a hit X has L = |X - o| <=
+// |o - c| + r + A L + b, so L <= 2.5 (...) while A <= 0.6), so the walk enters
+// it only if the ray meets the box thickened by rho_x(cull(best)) — after the
+// rest of the world has set `best`, a floor behind the mesh or a light the ray
+// passes far from costs one box test instead of a transform and a BLAS walk.
+// A > 0.6 (no cap) or no finite value: +inf (entered).
+struct NfWild {
+  float mn[3], mx[3];  // the instance's world box (nf_tree.cpp object_box)
+  float a0, a1, b0, b1;
+  float c[3], r;
+};
+MRT_HD float nf_rho_wild(const NfWild& x, V3 o, float d2, float t) {
+  const float dl = nf_sqrt_up(d2);
+  const float A = x.a0 + x.a1 * dl;
+  if (!(A <= 0.6f)) return INFINITY;
+  const float b = x.b0 + x.b1 * nf_len(o);
+  const float dist = nf_len(V3{o.x - x.c[0], o.y - x.c[1], o.z - x.c[2]}) + x.r;
+  const float r = fmaf(A, fminf(dl * t, 2.5f * (dist + b)), b) * (1.0f + 0x1p-16f);
+  return r <= 0x1p100f ? r : INFINITY;  // NaN (an infinite origin) or huge: entered
+}
+// Does the ray (o, d) meet the wild box thickened by rho = nf_rho_wild(x, o,
+// |d|^2, tmax) at some t in [tmin, tmax]? Planes moved out by rho and by an
+// ulp (the rounding of plane -/+ rho), IEEE quotients (plane - o) / d, each
+// entry lowered and exit raised by 2^-21 relative (the subtraction's and the
+// division's roundings, 2.01u, with slack) plus 2^-140 (underflow); a
+// direction component of zero: the slab holds all t or none. False only for
+// a certain miss.
+MRT_HD bool nf_wild_hit(const NfWild& x, V3 o, V3 d, float d2, float tmin, float tmax) {
+  const float rho = nf_rho_wild(x, o, d2, tmax);
+  if (!(rho < INFINITY)) return true;
+  float t0 = tmin, t1 = tmax;
+  const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+  for (int k = 0; k < 3; ++k) {
+    float pl = x.mn[k] - rho, ph = x.mx[k] + rho;
+    pl -= fmaf(fabsf(pl), 0x1p-23f, 0x1p-140f);
+    ph += fmaf(fabsf(ph), 0x1p-23f, 0x1p-140f);
+    float en, ex;
+    if (dd[k] == 0.0f) {
+      const bool in = pl <= oo[k] && oo[k] <= ph;
+      en = in ? -INFINITY : INFINITY;
+      ex = in ? INFINITY : -INFINITY;
+    } else {
+      const float a = (pl - oo[k]) / dd[k], b = (ph - oo[k]) / dd[k];
+      en = fminf(a, b);
+      ex = fmaxf(a, b);
+      en -= fmaf(fabsf(en), 0x1p-21f, 0x1p-140f);
+      ex += fmaf(fabsf(ex), 0x1p-21f, 0x1p-140f);
+    }
+    t0 = fmaxf(t0, en);
+    t1 = fminf(t1, ex);
+  }
+  return !(t1 < t0);
+}
+
 }  // namespace mrt

@@ -150,13 +150,13 @@ TriBound tri_bound(const float ab[3], const float ac[3]) {
 struct Item {
   Box b;
   uint32_t rec;       // the item's record in the reference stream
-  bool wild = false;  // never culled (nf_tree.cpp wild()): the nodes on its path force their child
+  bool wild = false;  // an instance under the wild margin (nf_bound.h nf_rho_wild): its path's nodes are flagged
 };
 struct Node {
   Box b;
   int32_t l = -1, r = -1;
   uint32_t first = 0, count = 0, axis = 0;
-  uint32_t force = 0;  // kNfForceL / kNfForceR: that child is never culled (wild instances)
+  uint32_t force = 0;  // kNfForceL / kNfForceR: that child's subtree holds a wild instance
   uint32_t lo = 0, hi = 0;  // the subtree's items [lo, hi) (build partitions them in place)
   // normal cone of the subtree's generic triangles (nf_bound.h nf_cone_rg):
   // c + 128 per axis, and the code {j (4 bits), k (3 bits)}
@@ -251,9 +251,9 @@ struct Tree {
     nodes[id].l = l, nodes[id].r = r, nodes[id].axis = (uint32_t)axis;
     return id;
   }
-  // every node forces its child whose subtree holds a wild item (the path
-  // from the root to each wild leaf is never culled); returns whether node
-  // n's subtree holds one
+  // every node flags its child whose subtree holds a wild item (the nodes on
+  // the path from the root to each wild leaf thicken their boxes by the wild
+  // margin too); returns whether node n's subtree holds one
   bool mark_forced(int32_t n) {
     Node& x = nodes[n];
     if (x.l < 0) {
@@ -394,6 +394,7 @@ struct Builder {
       case KIND_MODEL:
         w[4 * at + 2] = next;
         patches.push_back({at, w[4 * r + 1]});  // the reference BLAS region it enters
+        if (wild_term.count(r)) wild_at.push_back({at, r});
         break;
       default: break;
     }
@@ -453,6 +454,10 @@ struct Builder {
   struct InstTerm {
     double w0, w1, b0, b1, ko;
   };
+  // wild instances: reference record -> (world box, instance term), and their
+  // NF leaf records (slot0.w patched to their WILD entry)
+  std::unordered_map<uint32_t, std::pair<Box, InstTerm>> wild_term;
+  std::vector<std::pair<uint32_t, uint32_t>> wild_at;  // (NF instance record, reference record)
 
   static void grow_bound(TriBound& m, const TriBound& b) {
     m.a0 = std::max(m.a0, b.a0), m.a1 = std::max(m.a1, b.a1), m.k1 = std::max(m.k1, b.k1);
@@ -754,6 +759,14 @@ struct Builder {
     double aw0 = 0, aw1 = 0, bw0 = 0, bw1 = 0, ko1 = 0, ao0 = 0, ao1 = 0, orad = 0;
     std::vector<Item> wild_items, items;
     Box gen_box;  // the world boxes of generic triangles (world, model or instanced): the a1 term's ball
+    // in a world of few instances, one whose absolute term exceeds 2^-14 (a
+    // 1000x floor's 4.6e-4: the rounding of its object-space origin, scaled
+    // back) is wild too (round 6): that term would thicken every node of the
+    // primitives' trees (mesh_ply's 1M triangles of 0.01), while a wild
+    // instance costs one box test of its own where the walk reaches it
+    uint32_t n_world_inst = 0;
+    for (uint32_t r : world_objs) n_world_inst += kind_of(w, r) == KIND_INST;
+    const bool few = n_world_inst <= kNfWildFew;
     for (uint32_t r : world_objs) {
       const uint32_t kd = kind_of(w, r);
       TriBound tb;
@@ -785,8 +798,9 @@ struct Builder {
           }
           ao0 = std::max(ao0, ob.a0), ao1 = std::max(ao1, ob.a1);
         }
-        if (wild(m)) {
+        if (wild(m) || (few && m.b0 > 0x1p-14)) {
           wild_items.push_back({b, r, true});
+          wild_term[r] = {b, m};
           s.nf_wild++;
           if (s.keep_nf_boxes) s.nf_inst_wild[w[4 * (size_t)r]] = 1;
           continue;
@@ -824,7 +838,7 @@ struct Builder {
       rr = f_up(std::sqrt(r2) * (1 + 0x1p-40));
     };
     // the a0 term's cap: a ball over the objects the world margin covers (the
-    // wild ones are never culled)
+    // wild ones have their own)
     Box wb;
     for (const Item& it : items) wb.grow(it.b);
     if (items.empty()) wb = world.nodes[0].b;
@@ -855,6 +869,21 @@ struct Builder {
       const uint32_t root = emit(blas[k]);
       if (root == ~0u) return (s.nf_note = "a box the node format cannot hold (not finite)", true);
       blas_root[s.blas_regions[k].begin] = root;
+    }
+    // each wild instance's WILD entry (layout.h, nf_bound.h NfWild): its
+    // world box, its own instance term, a ball holding the box
+    for (auto& [at, r] : wild_at) {
+      const auto& [b, m] = wild_term.at(r);
+      bool finite = true;
+      for (int k = 0; k < 3; ++k) finite = finite && std::fabs(b.mn[k]) < INFINITY && std::fabs(b.mx[k]) < INFINITY;
+      if (!finite) continue;  // no entry: the instance is entered whenever its forced path is walked
+      float c[3], rr;
+      ball(b, c, rr);
+      const uint32_t e = push(f2u(b.mn[0]), f2u(b.mn[1]), f2u(b.mn[2]), f2u(b.mx[0]));
+      push(f2u(b.mx[1]), f2u(b.mx[2]), f2u(f_up(m.w0)), f2u(f_up(m.w1)));
+      push(f2u(f_up(m.b0 + 0x1p-90)), f2u(f_up(m.b1)), f2u(c[0]), f2u(c[1]));
+      push(f2u(c[2]), f2u(rr), 0, 0);
+      w[4 * (size_t)at + 3] = e;
     }
     for (auto& [rec, ref_blas] : patches) {
       auto it = blas_root.find(ref_blas);

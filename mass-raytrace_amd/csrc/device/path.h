@@ -903,7 +903,8 @@ MRT_DEV void nf_finish(const TravIn& in, Trav& t, LocalCounters& lc) {
 // one: the walk's boxes may be loose (its hits are checked against the
 // reference tree), never tight. Other rays: the exact test on the decoded
 // planes moved out by rho and widened by an ulp. A child whose force bit is
-// set (kNfForceL/R) is never culled.
+// set (kNfForceL/R: a wild instance below, nf_bound.h NfWild) is never culled
+// here; the wild instance's own leaf test decides (trav_prim_index_nf).
 MRT_DEV void nf_node_test(const uint4& s0, const uint4& s1, const TRay& r, float tmin, float tmax, float nfm, bool hit[2],
                           float ent[2], float ex[2]) {
   const V3 o{u2f(s0.x), u2f(s0.y), u2f(s0.z)};
@@ -993,6 +994,17 @@ MRT_DEV void trav_box_index_nf(const TravIn& in, const NfStack& k, Trav& t, Loca
   }
 }
 
+// A wild instance's leaf record (slot0.w: its WILD entry, layout.h): does the
+// world ray meet its world box thickened by its own margin at [tmin,
+// cull(best)]? (nf_bound.h NfWild; the nodes above it never cull it)
+MRT_DEV bool nf_wild_enter(const TravIn& in, const Trav& t, uint32_t at) {
+  const uint4 a = rec_load1<false>(in, at), b = rec_load1<false>(in, at + 1), c = rec_load1<false>(in, at + 2),
+              e = rec_load1<false>(in, at + 3);
+  const NfWild x{{u2f(a.x), u2f(a.y), u2f(a.z)}, {u2f(a.w), u2f(b.x), u2f(b.y)}, u2f(b.z), u2f(b.w), u2f(c.x), u2f(c.y),
+                 {u2f(c.z), u2f(c.w), u2f(e.x)}, u2f(e.y)};
+  return nf_wild_hit(x, t.r.o, t.r.d, t.r.a.b, in.tmin, nf_cull(t.best));
+}
+
 // The current record is an NF leaf's primitive, instance or model.
 template <bool COUNT, uint32_t ALPHA>
 MRT_DEV void trav_prim_index_nf(const TravIn& in, const NfStack& k, Trav& t, LocalCounters& lc) {
@@ -1018,6 +1030,8 @@ MRT_DEV void trav_prim_index_nf(const TravIn& in, const NfStack& k, Trav& t, Loc
     if (sphere_hit(V3{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, u2f(s0.w), t.r.o, t.r.d, t.r.a, in.tmin, nf_cull(t.best), th))
       nf_hit(in, t, th, make_ref(MRT_REF_SPHERE, s1.x));
     next = s1.y;
+  } else if (kind == KIND_INST && s0.w != 0 && !nf_wild_enter(in, t, s0.w)) {
+    next = s0.z;  // a wild instance the ray passes by (its own box and margin)
   } else {  // KIND_INST / KIND_MODEL: enter its BLAS, come back to the leaf's next record
     if (s0.z != kNfPop) nf_push(k, t, s0.z);
     nf_push(k, t, kNfRet);

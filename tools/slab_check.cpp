@@ -75,6 +75,8 @@ float margin(const Ray& r, float t0, float t1) { return std::fma(fabsf(t0) + fab
 struct Stats {
   uint64_t boxes = 0, undecided = 0, wrong = 0;
   uint64_t loads = 0;  // 16-B record loads (k_trace's vector-memory instructions per lane step)
+  uint64_t entries = 0;  // instance entries (each: a transform, the object margin, the world ray back)
+  uint64_t wild_skips = 0;  // wild instances passed by on their own box test
 };
 // path.h box_hit_any's early decision: 1 hit, 0 miss, -1 left to the exact test
 int early_decide(const float mn[3], const float mx[3], const Ray& r, float tmin, float best) {
@@ -132,10 +134,17 @@ const float kTmin = 0.001f;
 // box in its own space, and an instance's hit within the world rho of the
 // instance's world box (unless it is wild: never culled)
 struct BoundCheck {
-  uint64_t checks = 0, outside = 0, over = 0;
-  double worst = 0, worst_cap = 0;  // max dist / rho, max L / L_cap
+  uint64_t checks = 0, outside = 0, over = 0, wild_checks = 0;
+  double worst = 0, worst_cap = 0, worst_wild = 0;  // max dist / rho, max L / L_cap, the wild margin's max dist / rho
 };
 BoundCheck* g_bc = nullptr;
+// instance id -> its WILD entry's first slot (nf_bound.h NfWild; 0: not wild)
+std::unordered_map<uint32_t, uint32_t> g_wild_entry;
+NfWild wild_entry(const HostScene& s, uint32_t at) {
+  const uint32_t* e = s.slots.data() + 4 * (size_t)at;
+  auto fl = [&](int i) { float v; memcpy(&v, &e[i], 4); return v; };
+  return NfWild{{fl(0), fl(1), fl(2)}, {fl(3), fl(4), fl(5)}, fl(6), fl(7), fl(8), fl(9), {fl(10), fl(11), fl(12)}, fl(13)};
+}
 
 // NF tree parents (normal cones, round 6): every node a primitive's test
 // passes through on the near-first walk thickens its boxes by that node's
@@ -174,6 +183,7 @@ void map_nf_tree(const HostScene& s, uint32_t root, std::vector<uint8_t>& seen_b
       } else if (b[7] == KIND_SPHERE) {
         next = b[5];
       } else {
+        if (b[7] == KIND_INST && b[3] != 0) g_wild_entry[b[0]] = b[3];
         if (!seen_blas[b[1]]) {
           seen_blas[b[1]] = 1;
           map_nf_tree(s, b[1], seen_blas);
@@ -230,6 +240,27 @@ void check_hit(const HostScene& s, const float* box, V o, V d, float t, bool obj
   // the cap: rho at the capped L must still cover this hit
   if (dist > cap) g_bc->over++;
 }
+// a wild instance's hit in world space against its world box, within the wild margin
+void check_hit_wild(const HostScene& s, uint32_t inst, V o, V d, float t) {
+  auto it = g_wild_entry.find(inst);
+  if (it == g_wild_entry.end()) return;  // no entry (an infinite box): always entered
+  const NfWild e = wild_entry(s, it->second);
+  const float box[6] = {e.mn[0], e.mn[1], e.mn[2], e.mx[0], e.mx[1], e.mx[2]};
+  const double x = (double)o.x + (double)t * d.x, y = (double)o.y + (double)t * d.y, z = (double)o.z + (double)t * d.z;
+  const mrt::V3 oo{o.x, o.y, o.z};
+  const float rho = nf_rho_wild(e, oo, dot(d, d), t), cap = nf_rho_wild(e, oo, dot(d, d), INFINITY);
+  const double dist = box_dist(box, x, y, z);
+  g_bc->checks++;
+  g_bc->wild_checks++;
+  if (dist > 0) g_bc->outside++;
+  const double ratio = dist / (double)rho;
+  if (ratio > 1 || dist > cap) {
+    if (g_bc->over < 5) fprintf(stderr, "wild bound exceeded: dist %.3e rho %.3e t %a\n", dist, (double)rho, t);
+    g_bc->over++;
+  }
+  g_bc->worst = std::max(g_bc->worst, ratio);
+  g_bc->worst_wild = std::max(g_bc->worst_wild, ratio);
+}
 const float* leaf_box(const HostScene& s, uint32_t base, uint32_t id) {
   if (s.nf_leaf_box.empty()) return nullptr;
   return &s.nf_leaf_box[6 * (size_t)(s.vnf_base[base] + id)];
@@ -282,7 +313,10 @@ Result walk_plain(const HostScene& s, V o, V d, Stats* st = nullptr) {
         check_hit(s, leaf_box(s, VNF_TRI, a[6] & kTriIdMask), r.o, r.d, t, inst, s.vnf_base[VNF_TRI] + (a[6] & kTriIdMask));
         if (inst) {  // the same hit in world space against the instance's world box
           const uint32_t cid = w[4 * (size_t)((ret & 0x7FFFFFFFu) - 2)];
-          if (s.nf_inst_wild.empty() || !s.nf_inst_wild[cid]) check_hit(s, leaf_box(s, VNF_INST, cid), wr.o, wr.d, t, false);
+          if (s.nf_inst_wild.empty() || !s.nf_inst_wild[cid])
+            check_hit(s, leaf_box(s, VNF_INST, cid), wr.o, wr.d, t, false);
+          else  // a wild instance: its world box within the wild margin (nf_bound.h nf_rho_wild)
+            check_hit_wild(s, cid, wr.o, wr.d, t);
         } else if (ret != ~0u) {  // a model's triangle: its world box too
           const uint32_t cid = w[4 * (size_t)(ret - 2)];
           check_hit(s, leaf_box(s, VNF_MODEL, cid), wr.o, wr.d, t, false);
@@ -291,7 +325,7 @@ Result walk_plain(const HostScene& s, V o, V d, Stats* st = nullptr) {
       i = a[11];  // next (layout.h)
     } else if (k == KIND_INST) {
       const float* m = &s.inst_inv[12 * (size_t)a[0]];
-      if (st) st->loads += 5;
+      if (st) st->loads += 5, st->entries++;
       r = make_ray(xf(m, wr.o, 1.0f), xf(m, wr.d, 0.0f), s.early_ok);
       ret = (i + 2) | 0x80000000u;
       i = a[1];
@@ -478,8 +512,14 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks, uin
       if (st) st->loads += 2;
       if (sphere_hit({f(a[0]), f(a[1]), f(a[2])}, f(a[3]), r.o, r.d, kTmin, cull(), t)) hit(t, pr);
       next = a[5];
+    } else if (k == KIND_INST && a[3] != 0 &&
+               !nf_wild_hit(wild_entry(s, a[3]), mrt::V3{r.o.x, r.o.y, r.o.z}, mrt::V3{r.d.x, r.d.y, r.d.z}, dot(r.d, r.d),
+                            kTmin, cull())) {
+      if (st) st->loads += 4, st->wild_skips++;  // path.h nf_wild_enter: the WILD entry, then the leaf's next
+      next = a[2];
     } else if (k == KIND_INST || k == KIND_MODEL) {
       if (st) st->loads += k == KIND_INST ? 5 : 2;
+      if (st && k == KIND_INST) st->entries++;
       if (a[2] != kNfPop) stack.push_back(a[2]), stack_nl.push_back(nl);
       stack.push_back(0x80000000u);
       stack_nl.push_back(nl);
@@ -609,6 +649,11 @@ int main(int argc, char** argv) {
     std::vector<uint8_t> seen(s.slots.size() / 4, 0);
     map_nf_tree(s, s.nf_world, seen);
     printf("%-14s nf cones: %u of %u nodes carry one, kc %.3g\n", argv[1], s.nf_cones, s.nf_boxes, (double)s.nfb.kc);
+    for (const auto& [inst, at] : g_wild_entry) {
+      const NfWild e = wild_entry(s, at);
+      printf("%-14s wild instance %u: box (%.4g %.4g %.4g)-(%.4g %.4g %.4g) a0 %.3g a1 %.3g b0 %.3g b1 %.3g r %.3g\n", argv[1],
+             inst, e.mn[0], e.mn[1], e.mn[2], e.mx[0], e.mx[1], e.mx[2], e.a0, e.a1, e.b0, e.b1, e.r);
+    }
   }
   uint64_t nf_bad = 0, nf_fallbacks = 0, nf_starts_ref = 0, nf_even = 0, nf_odd = 0;
   BoundCheck bc;
@@ -736,7 +781,12 @@ int main(int argc, char** argv) {
            "%llu rays start on the reference walk (%.2f%%), %u wild instances\n",
            argv[1], (unsigned long long)bc.checks, (unsigned long long)bc.outside, bc.worst,
            (unsigned long long)bc.over, (unsigned long long)nf_starts_ref, 100.0 * nf_starts_ref / n, s.nf_wild);
-    printf("%-14s nf box tests per ray: even rays %.1f, odd rays %.1f\n", argv[1], 2.0 * nf_even / n, 2.0 * nf_odd / n);
+    printf("%-14s nf box tests per ray: even rays %.1f, odd rays %.1f; instance entries per ray %.3f\n", argv[1],
+           2.0 * nf_even / n, 2.0 * nf_odd / n, (double)nf_st.entries / n);
+    printf("%-14s nf wild instances passed by per ray %.3f\n", argv[1], (double)nf_st.wild_skips / n);
+    printf("%-14s reference walk: instance entries per ray %.3f\n", argv[1], (double)st.entries / n);
+    printf("%-14s nf wild: %llu hits of wild instances checked, worst dist/rho %.3g\n", argv[1],
+           (unsigned long long)bc.wild_checks, bc.worst_wild);
     if (bc.over) return 1;
     if (nf_bad) return 1;
   }
