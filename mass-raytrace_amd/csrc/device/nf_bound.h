@@ -47,6 +47,11 @@ struct NfBound {
   // triangles' normals lie in the cone (c, chi) and whose |c| M <= 2^(k+6);
   // 0: the scene's trees carry no cones (no generic triangles)
   float kc;
+  // a node's cone is evaluated only while some lane of the wave has a generic
+  // term rg t above this (2^-6 of the median generic triangle's extent): a
+  // bounce ray's short reach leaves the worst-case term small (path.h
+  // trav_box_index_nf; either value is a valid rho)
+  float kcmin;
 };
 
 // The walk is run only when the generic-triangle kappa stays at most
@@ -77,6 +82,18 @@ MRT_HD float nf_sqrt_up(float x) {
 #endif
 }
 MRT_HD float nf_len(V3 v) { return nf_sqrt_up((v.x * v.x + v.y * v.y) + v.z * v.z); }
+// min of two arithmetic results (never a signalling NaN): on the device one
+// v_min_f32 — fminf would first canonicalise each operand (v_max x, x), a
+// per-node cost of the margin
+MRT_HD float nf_min(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return fminf(a, b);
+#endif
+}
 
 // may this ray (world space, |d|^2 = d2) take the near-first walk?
 MRT_HD bool nf_ray_ok(const NfBound& B, float d2) {
@@ -141,7 +158,7 @@ MRT_HD NfLine nf_line(const NfBound& B, const NfCoef& c, float cb, float a0, flo
                 fmaf(k, c.delta, c.b) * up, B.kc * d2 * up, c.dl, 128.0f * ((d.x + d.y) + d.z)};
 }
 // (a nearer cull bound cb' < cb keeps the line and caps it at nf_rho_node(l, cb'))
-MRT_HD float nf_rho_node(const NfLine& l, float t) { return fminf(l.rcb, fmaf(l.ra0 + l.rg, t, l.rb)); }
+MRT_HD float nf_rho_node(const NfLine& l, float t) { return nf_min(l.rcb, fmaf(l.ra0 + l.rg, t, l.rb)); }
 
 // ---- normal cones (round 6; DESIGN.md §4 "Normal cones") ----
 // The generic-triangle term comes from Moller-Trumbore's cancellation, which
@@ -173,11 +190,11 @@ MRT_HD float nf_cone_rg(const NfLine& l, uint32_t ox, uint32_t oy, uint32_t oz, 
 #else
   const float rcp = 1.0f / fmaxf(G, 0x1p-100f);
 #endif
-  return fminf(l.rg, ldexpf(l.kd, (int)(code >> 4)) * rcp);
+  return nf_min(l.rg, ldexpf(l.kd, (int)(code >> 4)) * rcp);
 }
 // rho of a node (record words o.x, o.y, o.z, w) for hits at t or before
 MRT_HD float nf_rho_cone(const NfLine& l, float t, uint32_t ox, uint32_t oy, uint32_t oz, uint32_t w, V3 d) {
-  return fminf(l.rcb, fmaf(l.ra0 + nf_cone_rg(l, ox, oy, oz, w, d), t, l.rb));
+  return nf_min(l.rcb, fmaf(l.ra0 + nf_cone_rg(l, ox, oy, oz, w, d), t, l.rb));
 }
 
 // ---- wild instances (round 6; DESIGN.md §4 "Wild instances") ----

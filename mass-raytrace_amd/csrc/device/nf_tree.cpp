@@ -457,6 +457,7 @@ struct Builder {
   // wild instances: reference record -> (world box, instance term), and their
   // NF leaf records (slot0.w patched to their WILD entry)
   std::unordered_map<uint32_t, std::pair<Box, InstTerm>> wild_term;
+  std::vector<float> gen_extent;  // each generic triangle's largest box extent (the cones' threshold, NfBound::kcmin)
   std::vector<std::pair<uint32_t, uint32_t>> wild_at;  // (NF instance record, reference record)
 
   static void grow_bound(TriBound& m, const TriBound& b) {
@@ -488,6 +489,7 @@ struct Builder {
         const float ab[3] = {u2f(q[3]), u2f(q[4]), u2f(q[5])}, ac[3] = {u2f(q[8]), u2f(q[9]), u2f(q[10])};
         const TriBound tbd = tri_bound(ab, ac);
         if (tb) grow_bound(*tb, tbd);
+        if (tbd.a1 > 0) gen_extent.push_back(std::max(b.mx[0] - b.mn[0], std::max(b.mx[1] - b.mn[1], b.mx[2] - b.mn[2])));
         pad_box(b, 0.0f);
         pad_abs(b, tbd.pad);
         break;
@@ -856,6 +858,11 @@ struct Builder {
     // roundings, and G's
     B.kc = (aw1 > 0 || ao1 > 0) ? f_up(1.0001 * 24.0 * kU * 64.0 / (1.0 - 1.01 * (double)kNfKappaMax) * (1.0 + 0x1p-17))
                                 : 0.0f;
+    B.kcmin = 0.0f;
+    if (!gen_extent.empty()) {
+      std::nth_element(gen_extent.begin(), gen_extent.begin() + gen_extent.size() / 2, gen_extent.end());
+      B.kcmin = std::ldexp(gen_extent[gen_extent.size() / 2], -6);
+    }
     if (r_max > 0) {
       ball(sph_box, B.sc, B.sr);
       B.s51 = f_up(51.2 * kU / r_min), B.s28 = f_up(27.8 * kU), B.s130 = f_up(130.2 * kU), B.s11 = f_up(11.2 * kU * r_max);

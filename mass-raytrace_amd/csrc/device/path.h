@@ -491,6 +491,12 @@ MRT_DEV float vmax3(float a, float b, float c) {
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
+// max(|a|, |b|, c) in one instruction (the abs as source modifiers)
+MRT_DEV float vmax3ab(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 
 // BoundingBox::hit (geom.rs:218-247): v_min = (min - o)/d, v_max = (max - o)/d,
 // six correctly rounded quotients — qfast in the ray's fast domain (bit-identical
@@ -912,50 +918,58 @@ MRT_DEV void nf_node_test(const uint4& s0, const uint4& s1, const TRay& r, float
               __uint_as_float(((s0.w >> 16) & 0xFFu) << 23)};
   const uint32_t qw[3] = {s1.x, s1.y, s1.z};
   auto q = [&](int j) { return (float)((qw[j >> 2] >> (8 * (j & 3))) & 0xFFu); };  // v_cvt_f32_ubyteN
+  // both paths leave floats only (entry, entry - exit, margin, exit bound):
+  // the hit flags are formed after the merge, so no lane mask is carried
+  // across it in vector registers
+  float t0[2], dt[2], m[2], xb[2];
   if (tray_fast(r)) {
     const float ax = sc.x * r.yx, ay = sc.y * r.yy, az = sc.z * r.yz;
     const float bx = fmaf(o.x, r.yx, -r.oyx), by = fmaf(o.y, r.yy, -r.oyy), bz = fmaf(o.z, r.yz, -r.oyz);
     const float lbx = fmaf(-nfm, r.yx, bx), lby = fmaf(-nfm, r.yy, by), lbz = fmaf(-nfm, r.yz, bz);
     const float hbx = fmaf(nfm, r.yx, bx), hby = fmaf(nfm, r.yy, by), hbz = fmaf(nfm, r.yz, bz);
-    const float mabs = fmaf(vmax1(vmax3(fabsf(lbx), fabsf(lby), fabsf(lbz)), vmax3(fabsf(hbx), fabsf(hby), fabsf(hbz))),
-                            0x1p-20f, fabsf(r.om));
+    const float mabs = fmaf(vmax3ab(lbx, lby, vmax3ab(lbz, hbx, vmax3ab(hby, hbz, 0.0f))), 0x1p-20f, fabsf(r.om));
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int b = 6 * c;
       const float lx = fmaf(q(b), ax, lbx), ly = fmaf(q(b + 1), ay, lby), lz = fmaf(q(b + 2), az, lbz);
       const float hx = fmaf(q(b + 3), ax, hbx), hy = fmaf(q(b + 4), ay, hby), hz = fmaf(q(b + 5), az, hbz);
-      const float t0 = vmax3(vmin1(lx, hx), vmin1(ly, hy), vmax1(vmin1(lz, hz), tmin));
+      t0[c] = vmax3(vmin1(lx, hx), vmin1(ly, hy), vmax1(vmin1(lz, hz), tmin));
       const float t1 = vmin3(vmax1(lx, hx), vmax1(ly, hy), vmin1(vmax1(lz, hz), tmax));
-      const float m = fmaf(fabsf(t0) + fabsf(t1), 0x1p-19f, mabs);
-      const bool force = (s1.w & (kNfForceL << c)) != 0;
-      hit[c] = !(t0 - t1 > m) || force;
-      ent[c] = t0;
-      // every hit in the thickened box has t <= this (m covers t1's error and
-      // this rounding); a forced child holds a wild instance, whose hits the
-      // world margin does not place inside the box: no exit bound below it
-      ex[c] = force ? INFINITY : fmaf(m, 2.0f, t1);
+      m[c] = fmaf(fabsf(t0[c]) + fabsf(t1), 0x1p-19f, mabs);
+      dt[c] = t0[c] - t1;
+      // every hit in the thickened box has t <= this (m covers t1's error and this rounding)
+      xb[c] = fmaf(m[c], 2.0f, t1);
     }
-    return;
+  } else {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int b = 6 * c;
+      auto lo = [&](float qq, float s, float org) {
+        const float p = fmaf(qq, s, org) - nfm;
+        return p - fmaf(fabsf(p), 0x1p-23f, 0x1p-140f);
+      };
+      auto hi = [&](float qq, float s, float org) {
+        const float p = fmaf(qq, s, org) + nfm;
+        return p + fmaf(fabsf(p), 0x1p-23f, 0x1p-140f);
+      };
+      const V3 mn{lo(q(b), sc.x, o.x), lo(q(b + 1), sc.y, o.y), lo(q(b + 2), sc.z, o.z)};
+      const V3 mx{hi(q(b + 3), sc.x, o.x), hi(q(b + 4), sc.y, o.y), hi(q(b + 5), sc.z, o.z)};
+      const V3 a = (mn - r.o) / r.d, bb = (mx - r.o) / r.d;  // IEEE quotients (the planes may lie outside the qfast domain)
+      t0[c] = vmax3(vmin1(a.x, bb.x), vmin1(a.y, bb.y), vmax1(vmin1(a.z, bb.z), tmin));
+      const float t1 = vmin3(vmax1(a.x, bb.x), vmax1(a.y, bb.y), vmin1(vmax1(a.z, bb.z), tmax));
+      dt[c] = t0[c] - t1;  // > 0 exactly when t1 < t0 (+-inf pairs: NaN, a hit as !(t1 < t0))
+      m[c] = 0.0f;
+      xb[c] = INFINITY;  // no exit bound from the exact quotients
+    }
   }
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
-    const int b = 6 * c;
-    auto lo = [&](float qq, float s, float org) {
-      const float p = fmaf(qq, s, org) - nfm;
-      return p - fmaf(fabsf(p), 0x1p-23f, 0x1p-140f);
-    };
-    auto hi = [&](float qq, float s, float org) {
-      const float p = fmaf(qq, s, org) + nfm;
-      return p + fmaf(fabsf(p), 0x1p-23f, 0x1p-140f);
-    };
-    const V3 mn{lo(q(b), sc.x, o.x), lo(q(b + 1), sc.y, o.y), lo(q(b + 2), sc.z, o.z)};
-    const V3 mx{hi(q(b + 3), sc.x, o.x), hi(q(b + 4), sc.y, o.y), hi(q(b + 5), sc.z, o.z)};
-    const V3 a = (mn - r.o) / r.d, bb = (mx - r.o) / r.d;  // IEEE quotients (the planes may lie outside the qfast domain)
-    const float t0 = vmax3(vmin1(a.x, bb.x), vmin1(a.y, bb.y), vmax1(vmin1(a.z, bb.z), tmin));
-    const float t1 = vmin3(vmax1(a.x, bb.x), vmax1(a.y, bb.y), vmin1(vmax1(a.z, bb.z), tmax));
-    hit[c] = !(t1 < t0) || (s1.w & (kNfForceL << c));
-    ent[c] = 0.0f;  // left first
-    ex[c] = INFINITY;
+    const bool force = (s1.w & (kNfForceL << c)) != 0;
+    hit[c] = !(dt[c] > m[c]) || force;
+    ent[c] = t0[c];
+    // a forced child holds a wild instance, whose hits the world margin does
+    // not place inside the box: no exit bound below it
+    ex[c] = force ? INFINITY : xb[c];
   }
 }
 
@@ -976,8 +990,12 @@ MRT_DEV void trav_box_index_nf(const TravIn& in, const NfStack& k, Trav& t, Loca
 #else
   // the node's normal cone narrows the generic-triangle term (nf_bound.h
   // nf_cone_rg); scenes without generic triangles (kc == 0) skip it
-  const float rho = in.S.nfb.kc > 0.0f ? nf_rho_cone(t.nfl, fminf(cb, t.nl), t.s0.x, t.s0.y, t.s0.z, t.s0.w, t.r.d)
-                                       : nf_rho_node(t.nfl, fminf(cb, t.nl));
+  // (the cones only while some lane's worst-case generic term is worth it:
+  // a wave-uniform choice, either rho is valid)
+  const float tn = vmin1(cb, t.nl);
+  float rho = nf_rho_node(t.nfl, tn);
+  if (in.S.nfb.kc > 0.0f && __builtin_amdgcn_ballot_w64(t.nfl.rg * tn > in.S.nfb.kcmin) != 0)
+    rho = nf_rho_cone(t.nfl, tn, t.s0.x, t.s0.y, t.s0.z, t.s0.w, t.r.d);
 #endif
   nf_node_test(t.s0, t.s1, t.r, in.tmin, cb, rho, h, e, x);
   const uint32_t base = t.s1.w & kNfIdx, right = base + 2u + ((t.s0.w >> 24) & 1u);  // lsz - 2 in bit 24 (layout.h)

@@ -475,8 +475,10 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks, uin
       bool h[2];
       float e[2], x[2];
       const float tn = fminf(cull(), nl);
-      const float rho = s.nfb.kc > 0 ? nf_rho_cone(nfl, tn, a[0], a[1], a[2], a[3], mrt::V3{r.d.x, r.d.y, r.d.z})
-                                     : nf_rho_node(nfl, tn);
+      // the cone while this ray's worst-case generic term is worth it (path.h: while some lane's is)
+      const float rho = s.nfb.kc > 0 && nfl.rg * tn > s.nfb.kcmin
+                            ? nf_rho_cone(nfl, tn, a[0], a[1], a[2], a[3], mrt::V3{r.d.x, r.d.y, r.d.z})
+                            : nf_rho_node(nfl, tn);
       node_test(a, r, kTmin, cull(), getenv("SLAB_NO_CONE") ? nf_rho_node(nfl, tn) : rho, h, e, x);
       const uint32_t base = k & kNfIdx, right = base + 2 + ((a[3] >> 24) & 1u);
       if (h[0] && h[1]) {
