@@ -379,11 +379,11 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  * DESIGN.md §4), so it meets every hit that can win and its closest hit is
  * the reference's, t bits and ties included; rays the bound does not cover
  * take the reference's walk. AUTO (the default) picks NEAR_FIRST unless the
- * bound has the generic-triangle term (large arbitrary triangles seen by
- * long camera rays: mesh_ply) or the world is a big instanced one (Menger),
- * where REFERENCE is faster. Measured round 5 (1080p x 1024 spp per step):
- * sphere_grid 976 vs 926, cube_field 504 vs 413 Msamples/s; mesh_ply 548 vs
- * 1148 and Menger 26 vs 50 (hence AUTO). Counters (node visits, ...) count
+ * world is a big instanced one (Menger), where REFERENCE is faster. Round 6
+ * (1080p x 1024 spp per step): sphere_grid 1152 vs 968, cube_field 563 vs
+ * 422, mesh_ply 1228 vs 1152 Msamples/s (normal cones bound the generic
+ * triangles' term per node; wild instances pass their own box test, nf_bound.h
+ * NfWild); Menger 26 vs 50 (hence AUTO). Counters (node visits, ...) count
  * the walk taken. */
 #define MRT_TRAVERSAL_AUTO (-1)
 #define MRT_TRAVERSAL_REFERENCE 0

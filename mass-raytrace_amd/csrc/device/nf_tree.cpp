@@ -685,16 +685,9 @@ struct Builder {
 
   // the per-scene rule's verdict before building (render.hip apply_options):
   // the reference walk for a generic-triangle term or a big instanced world
-  bool auto_declines() const {
-    if (d.n_instances > 1000 && (size_t)n_slots() * 16 > ((size_t)16 << 20)) return true;
-    for (uint32_t r : s.rec_starts)  // any generic triangle (tri_bound) among the records
-      if (kind_of(w, r) == KIND_TRI) {
-        const float ab[3] = {u2f(w[4 * (size_t)r + 3]), u2f(w[4 * (size_t)r + 4]), u2f(w[4 * (size_t)r + 5])};
-        const float ac[3] = {u2f(w[4 * (size_t)r + 8]), u2f(w[4 * (size_t)r + 9]), u2f(w[4 * (size_t)r + 10])};
-        if (tri_bound(ab, ac).a1 > 0) return true;
-      }
-    return false;
-  }
+  // (round 6: generic triangles no longer decline it — the normal cones and
+  // the wild instances' own tests made mesh_ply's near-first walk the faster)
+  bool auto_declines() const { return d.n_instances > 1000 && (size_t)n_slots() * 16 > ((size_t)16 << 20); }
 
   bool run() {
     s.nf_ok = false;
@@ -702,8 +695,8 @@ struct Builder {
     if (s.trav_rng) return (s.nf_note = "the traversal draws random numbers (Volume, Mix alpha)", true);
     if (s.nf_build == kNfBuildNever) return (s.nf_note = "not built (option traversal = REFERENCE at upload)", true);
     if (s.nf_build == kNfBuildAuto && auto_declines())
-      return (s.nf_note = "not built: the per-scene rule walks the reference's way (generic triangles or a big "
-                          "instanced world; option traversal = NEAR_FIRST at upload builds them)", true);
+      return (s.nf_note = "not built: the per-scene rule walks the reference's way (a big instanced world; "
+                          "option traversal = NEAR_FIRST at upload builds them)", true);
     s.vnf_base[VNF_SPHERE] = 0;
     s.vnf_base[VNF_TRI] = d.n_spheres;
     s.vnf_base[VNF_INST] = d.n_spheres + d.n_triangles;

@@ -1278,7 +1278,6 @@ struct mrt_ctx {
   int shade_wpe = 8;               // k_shade register budget: 8 or 7 waves/SIMD (option "shade_waves")
   uint32_t tl_boxes = 0;           // box records in the treelet
   bool scene_nf = false;           // the scene has verified near-first trees (nf_tree.cpp)
-  bool scene_nf_gen = false;       // their rounding margin has a generic-triangle term (nf_bound.h aw1 / ko1)
   std::string nf_note;             // why it has none
   bool use_nf = false;             // k_trace walks them (option "traversal", the scene, no treelet)
   int shade_bin = 0;                        // k_shade groups its survivors by material kind and direction (option "shade_bin")
@@ -1395,12 +1394,13 @@ void apply_options(mrt_ctx* c) {
   const int64_t* o = c->opt;
   const bool inst = c->scene_instances > 1000, big = c->scene_big;
   c->treelet_kb = (uint32_t)o[OPT_TREELET_KB];
-  // traversal -1 (per scene): the near-first walk unless its margin has the
-  // generic-triangle term (mesh_ply 548 vs 1148 Msamples/s: |det| >= 1e-6
-  // bounds Moller-Trumbore's rounding only loosely for camera rays, whose
-  // |d| is ~9) or the world is a big instanced one (Menger 25.7 / 45.9 at
-  // trace_nf_batch 64 vs 50.0); profiles/r5_walk_ab/
-  const bool nf_rule = !c->scene_nf_gen && !(inst && big);
+  // traversal -1 (per scene): the near-first walk unless the world is a big
+  // instanced one (Menger 25.7 / 45.9 at trace_nf_batch 64 vs 50.0;
+  // profiles/r5_walk_ab/). Round 5 also declined a margin with the generic-
+  // triangle term (mesh_ply 548 vs 1148: |det| >= 1e-6 priced for every
+  // ray); the normal cones and the wild instances' own tests turned that
+  // around (mesh_ply 1228 vs 1152, profiles/r6_wild/)
+  const bool nf_rule = !(inst && big);
   c->use_nf = (o[OPT_TRAVERSAL] == MRT_TRAVERSAL_NEAR_FIRST || (o[OPT_TRAVERSAL] < 0 && nf_rule)) && c->scene_nf &&
               !c->trace_lds && !c->scene_rng;
   const bool nf = c->use_nf, big_solid = big && !inst;
@@ -2323,7 +2323,6 @@ int mrt_upload_scene(mrt_ctx* c, const mrt_scene_desc* d) {
     c->scene_rng = hs.trav_rng;
     c->scene_ext = !hs.surf_ops.empty() || hs.bg_kind == MRT_BG_CUBEMAP;
     c->scene_nf = hs.nf_ok;
-    c->scene_nf_gen = hs.nf_ok && (hs.nfb.kw1 > 0.0f || hs.nfb.ko1 > 0.0f);
     c->nf_note = hs.nf_ok ? "" : hs.nf_note;
     apply_options(c);  // the per-scene rules of the options left at -1
     c->has_scene = true;

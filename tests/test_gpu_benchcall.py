@@ -2,8 +2,8 @@
 1920x1080x1024 spp with the default options — G = 2,123,366,400 samples in
 one call: the default 2^31-sample results slab (98.9% full), the default path
 pool refilled hundreds of times, the drain hand-off, and the per-scene walk
-(AUTO: the proven near-first walk on sphere_grid and cube_field, the
-reference's walk on mesh_ply) — checked on a ~200-pixel subset against the
+(AUTO: the proven near-first walk on all three since round 6; mesh_ply
+also on the reference's walk, option traversal = 0) — checked on a ~200-pixel subset against the
 oracle at the same 1024 spp: bounce counts bit-exact, radiance within 1e-4
 relative L2 (paths are per-(pixel, sample) independent, so the oracle
 recomputes any subset exactly; bench.py step: massrt.Image.render + gather).
@@ -27,15 +27,17 @@ def _pixels(n=200, seed=5):
     return px.astype(np.uint32)
 
 
-@pytest.mark.parametrize("scene", ["sphere_grid", "mesh_ply", "cube_field"])
-def test_bench_call_matches_oracle(golden_dir, assets_dir, scene):
+@pytest.mark.parametrize("scene,walk", [("sphere_grid", "auto"), ("mesh_ply", "auto"), ("cube_field", "auto"),
+                                        ("mesh_ply", "reference")])
+def test_bench_call_matches_oracle(golden_dir, assets_dir, scene, walk):
     src = assets_dir if scene == "mesh_ply" else golden_dir
     b = massrt.Builder(1).builtin(scene, ASPECT, src)
-    c = massrt.Context(0)  # default options: what bench.py's headline and secondary lines run
+    # default options (what bench.py's headline and secondary lines run), or the reference's walk
+    c = massrt.Context(0, options={} if walk == "auto" else {"traversal": massrt.TRAVERSAL_REFERENCE})
     try:
         c.upload(b)
-        walk = c.tuning()["traversal"]
-        assert walk == (massrt.TRAVERSAL_REFERENCE if scene == "mesh_ply" else massrt.TRAVERSAL_NEAR_FIRST)
+        taken = c.tuning()["traversal"]
+        assert taken == (massrt.TRAVERSAL_REFERENCE if walk == "reference" else massrt.TRAVERSAL_NEAR_FIRST)
         img = massrt.Image(c, W, H)
         img.render(1, 0, SPP)  # one call: the whole 1024-spp frame (bench.py RankRunner.step)
         img.gather()
