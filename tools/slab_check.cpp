@@ -77,6 +77,7 @@ struct Stats {
   uint64_t loads = 0;  // 16-B record loads (k_trace's vector-memory instructions per lane step)
   uint64_t entries = 0;  // instance entries (each: a transform, the object margin, the world ray back)
   uint64_t wild_skips = 0;  // wild instances passed by on their own box test
+  uint64_t prims = 0;       // primitive tests
 };
 // path.h box_hit_any's early decision: 1 hit, 0 miss, -1 left to the exact test
 int early_decide(const float mn[3], const float mx[3], const Ray& r, float tmin, float best) {
@@ -503,7 +504,7 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks, uin
     if (k == KIND_TRI) {
       float t;
       const uint32_t pr = MRT_REF(MRT_REF_TRIANGLE, a[6] & kTriIdMask);
-      if (st) st->loads += 3;
+      if (st) st->loads += 3, st->prims++;
       if (tri_hit({f(a[0]), f(a[1]), f(a[2])}, {f(a[3]), f(a[4]), f(a[5])}, {f(a[8]), f(a[9]), f(a[10])}, r.o, r.d,
                   kTmin, cull(), t))
         hit(t, pr);
@@ -511,7 +512,7 @@ Result walk_nf(const HostScene& s, V o, V d, Stats* st, uint64_t* fallbacks, uin
     } else if (k == KIND_SPHERE) {
       float t;
       const uint32_t pr = MRT_REF(MRT_REF_SPHERE, a[4]);
-      if (st) st->loads += 2;
+      if (st) st->loads += 2, st->prims++;
       if (sphere_hit({f(a[0]), f(a[1]), f(a[2])}, f(a[3]), r.o, r.d, kTmin, cull(), t)) hit(t, pr);
       next = a[5];
     } else if (k == KIND_INST && a[3] != 0 &&
@@ -785,7 +786,9 @@ int main(int argc, char** argv) {
            (unsigned long long)bc.over, (unsigned long long)nf_starts_ref, 100.0 * nf_starts_ref / n, s.nf_wild);
     printf("%-14s nf box tests per ray: even rays %.1f, odd rays %.1f; instance entries per ray %.3f\n", argv[1],
            2.0 * nf_even / n, 2.0 * nf_odd / n, (double)nf_st.entries / n);
-    printf("%-14s nf wild instances passed by per ray %.3f\n", argv[1], (double)nf_st.wild_skips / n);
+    printf("%-14s nf wild instances passed by per ray %.3f; primitive tests per ray %.2f; cost estimate %.0f VALU/ray "
+           "(58 per box test, 45 per primitive test, 500 per instance entry)\n", argv[1], (double)nf_st.wild_skips / n,
+           (double)nf_st.prims / n, (58.0 * nf_st.boxes + 45.0 * nf_st.prims + 500.0 * nf_st.entries) / n);
     printf("%-14s reference walk: instance entries per ray %.3f\n", argv[1], (double)st.entries / n);
     printf("%-14s nf wild: %llu hits of wild instances checked, worst dist/rho %.3g\n", argv[1],
            (unsigned long long)bc.wild_checks, bc.worst_wild);
