@@ -79,7 +79,9 @@ constexpr uint32_t kTriIdMask = 0x0FFFFFFFu;
 //           stream's box record decides one): half the vector loads per box.
 //   SPHERE / TRI as in the reference stream, `next` = the leaf's following
 //           record or kNfPop (continue with the stack)
-//   INST / MODEL {id, nf_blas_root, next, 0} {0,0,0,INST|MODEL}
+//   INST / MODEL {id, nf_blas_root, next, wild} {parent, 0, 0, INST|MODEL}
+//           wild: a wild instance's WILD entry (nf_bound.h NfWild), else 0;
+//           parent: its reference world parent box (vnf_leaf's, for nf_finish)
 constexpr uint32_t kNfIdx = 0x0FFFFFFFu;  // index bits of an NF node's children base
 // an NF node's slot1.w: its left / right child's subtree holds a "wild"
 // instance, whose rounding the world margin does not cover (nf_tree.cpp): the

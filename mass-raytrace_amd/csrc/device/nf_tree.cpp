@@ -393,6 +393,7 @@ struct Builder {
       case KIND_INST:
       case KIND_MODEL:
         w[4 * at + 2] = next;
+        w[4 * (at + 1)] = s.vnf_leaf[2 * (size_t)vnf_slot(r)];  // its reference world parent (path.h nf_finish)
         patches.push_back({at, w[4 * r + 1]});  // the reference BLAS region it enters
         if (wild_term.count(r)) wild_at.push_back({at, r});
         break;

@@ -869,8 +869,11 @@ MRT_DEV void nf_finish(const TravIn& in, Trav& t, LocalCounters& lc) {
       if (own != kNoParent) ok = ref_box_hits(in, own, t.r, tau);
     } else {
       const bool inst = (t.hit_ret & kRetInstance) != 0;
-      const uint32_t cid = in.slots[MRT_IDX(S, (t.hit_ret & ~kRetInstance) - 2, S.n_slots, 24)].x;
-      const uint32_t wpar = vnf_entry(S, inst ? VNF_INST : VNF_MODEL, cid, 0);
+      // the NF instance/model record holds its id and its reference world
+      // parent (layout.h): one load pair, not id -> vnf_leaf -> parent
+      uint4 ra, rb;
+      rec_load2<false>(in, (t.hit_ret & ~kRetInstance) - 2, ra, rb);
+      const uint32_t cid = ra.x, wpar = rb.x;
       if (wpar != kNoParent) ok = ref_box_hits(in, wpar, t.r, tau);
       if (ok && own != kNoParent) {
         TRay r = t.r;

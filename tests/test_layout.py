@@ -94,7 +94,7 @@ def _wild_checked(stdout: str, n_wild: int):
     line = [x for x in stdout.splitlines() if " nf wild: " in x][0]
     assert int(line.split("nf wild: ")[1].split(" hits")[0]) > 100, line
     assert float(line.split("worst dist/rho ")[1]) < 0.25, line
-    passed = float(stdout.split("nf wild instances passed by per ray ")[1].split()[0])
+    passed = float(stdout.split("nf wild instances passed by per ray ")[1].split()[0].rstrip(";"))
     assert passed > 0.1, stdout
 
 
