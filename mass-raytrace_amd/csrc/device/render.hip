@@ -1387,7 +1387,8 @@ void set_device(mrt_ctx* c) { HIP_CHECK(hipSetDevice(c->device)); }
 //  The near-first walk (round 4, profiles/r4_nf/tune.txt) has rules of its
 //  own: refill 40 except for a big non-instanced world (sphere_grid 1106.9
 //  -> 1137.4, cube_field 608.6 -> 614.6; mesh_ply 1581.6 -> 1528.7 keeps 32)
-//  and box run >= 28 lanes there, 512 rays per grab except there (cube_field
+//  and box run >= 20 lanes without many instances (round 6, profiles/r6_knobs/:
+//  mesh_ply 1213 -> 1252 from 28, sphere_grid 1155 -> 1164 from 24), 512 rays per grab except there (cube_field
 //  556.2 -> 580.2 with shade 7; mesh_ply keeps 128: 1386.7 vs 1372.7), and
 //  k_shade at 7 waves/SIMD everywhere (sphere_grid 983.3 -> 992.9).
 void apply_options(mrt_ctx* c) {
@@ -1412,7 +1413,7 @@ void apply_options(mrt_ctx* c) {
   c->tune.refill = o[OPT_TRACE_REFILL] >= 0 ? (uint32_t)std::max<int64_t>(1, o[OPT_TRACE_REFILL])
                                             : ((nf && !big_solid) ? 40u : (inst && big) ? 12u : 32u);
   c->tune.box_min = o[OPT_TRACE_BOX_MIN] >= 0 ? (uint32_t)std::max<int64_t>(1, o[OPT_TRACE_BOX_MIN])
-                                              : (inst ? 16u : (big ? (nf ? 28u : 32u) : 24u));
+                                              : (inst ? 16u : (nf ? 20u : (big ? 32u : 24u)));
   c->tune.chunk = o[OPT_TRACE_CHUNK] >= 0 ? (uint32_t)o[OPT_TRACE_CHUNK]
                                           : (nf ? (big_solid ? 128u : 512u) : ((big || inst) ? 128u : 512u));
   c->tune.prim_batch = (uint32_t)o[OPT_TRACE_PRIM_BATCH];

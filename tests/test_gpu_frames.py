@@ -240,7 +240,7 @@ def test_options_and_tuning(scene, golden_dir):
     t = c.tuning()
     # traversal AUTO: sphere_grid takes the near-first walk (its own rules: refill 40, k_shade at 7)
     assert c.get_option("traversal") == massrt.TRAVERSAL_AUTO and t["traversal"] == massrt.TRAVERSAL_NEAR_FIRST
-    assert t["queues"] == 2 and t["trace_box_min"] == 24 and t["trace_chunk"] == 512 and t["shade_waves"] == 7
+    assert t["queues"] == 2 and t["trace_box_min"] == 20 and t["trace_chunk"] == 512 and t["shade_waves"] == 7
     assert t["shade_bin"] == 2 and c.get_option("shade_bin") == -1  # grouped survivors, pool split by y sign (near-first)
     c.set_option("shade_bin", 0)
     assert c.tuning()["shade_bin"] == 0
