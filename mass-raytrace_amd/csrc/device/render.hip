@@ -1387,6 +1387,7 @@ void set_device(mrt_ctx* c) { HIP_CHECK(hipSetDevice(c->device)); }
 //  The near-first walk (round 4, profiles/r4_nf/tune.txt) has rules of its
 //  own: refill 40 except for a big non-instanced world (sphere_grid 1106.9
 //  -> 1137.4, cube_field 608.6 -> 614.6; mesh_ply 1581.6 -> 1528.7 keeps 32)
+//  (round 6: a big solid world grabs 256, mesh_ply 1274 -> 1290; profiles/r6_knobs/)
 //  and box run >= 20 lanes without many instances (round 6, profiles/r6_knobs/:
 //  mesh_ply 1213 -> 1252 from 28, sphere_grid 1155 -> 1164 from 24), 512 rays per grab except there (cube_field
 //  556.2 -> 580.2 with shade 7; mesh_ply keeps 128: 1386.7 vs 1372.7), and
@@ -1415,7 +1416,7 @@ void apply_options(mrt_ctx* c) {
   c->tune.box_min = o[OPT_TRACE_BOX_MIN] >= 0 ? (uint32_t)std::max<int64_t>(1, o[OPT_TRACE_BOX_MIN])
                                               : (inst ? 16u : (nf ? 20u : (big ? 32u : 24u)));
   c->tune.chunk = o[OPT_TRACE_CHUNK] >= 0 ? (uint32_t)o[OPT_TRACE_CHUNK]
-                                          : (nf ? (big_solid ? 128u : 512u) : ((big || inst) ? 128u : 512u));
+                                          : (nf ? (big_solid ? 256u : 512u) : ((big || inst) ? 128u : 512u));
   c->tune.prim_batch = (uint32_t)o[OPT_TRACE_PRIM_BATCH];
   c->tune.nf_batch = o[OPT_TRACE_NF_BATCH] > 0 ? (uint32_t)o[OPT_TRACE_NF_BATCH] : c->tune.refill;
   c->tune.shade_batch = (uint32_t)o[OPT_SHADE_BATCH];
