@@ -157,8 +157,8 @@ MRT_DEV V4 surface_get_f(const DevScene& S, const GpuMaterial& m, V2 uv, LocalCo
 }
 
 // ---- primitive tests -------------------------------------------------------
-// Correctly rounded quotient a/b from y = RN(1/b) (computed once per ray with
-// a true IEEE division): q0 = a*y can be ~2 ulp off; one FMA residual
+// Correctly rounded quotient a/b from y = RN(1/b) (computed once per ray,
+// rcp_cr: exactly the IEEE 1/b): q0 = a*y can be ~2 ulp off; one FMA residual
 // correction makes it faithful and a second rounds it exactly (Markstein's
 // theorem: y within 1/2 ulp of 1/b + faithful q => RN(q + (a - bq)y) = RN(a/b),
 // absent under/overflow). Results outside [2^-90, 2^90], dividends below
@@ -171,7 +171,7 @@ struct Recip {
 MRT_DEV Recip make_recip(float b) {
   Recip r;
   r.b = b;
-  r.y = 1.0f / b;
+  r.y = rcp_cr(b);
   return r;
 }
 // divisor inside the fast path's range
@@ -238,9 +238,9 @@ MRT_DEV TRay make_tray(V3 o, V3 d, uint32_t scene_flags) {
   TRay r;
   r.o = o;
   r.d = d;
-  r.yx = 1.0f / d.x;
-  r.yy = 1.0f / d.y;
-  r.yz = 1.0f / d.z;
+  r.yx = rcp_cr(d.x);
+  r.yy = rcp_cr(d.y);
+  r.yz = rcp_cr(d.z);
   r.oyx = o.x * r.yx;
   r.oyy = o.y * r.yy;
   r.oyz = o.z * r.yz;
@@ -282,7 +282,7 @@ MRT_DEV bool tri_hit(V3 a, V3 ab, V3 ac, V3 o, V3 d, float tmin, float tmax, flo
   V3 p_vec = cross(d, ac);
   float det = dot(ab, p_vec);
   if (fabsf(det) < 0.000001f) return false;
-  float inv_det = 1.0f / det;
+  float inv_det = rcp_cr(det);  // RN(1 / det), as the reference's 1.0 / det
   V3 t_vec = o - a;
   float u = dot(t_vec, p_vec) * inv_det;
   if (u < 0.0f || u > 1.0f) return false;
@@ -774,24 +774,28 @@ MRT_DEV void nf_start(const TravIn& in, Trav& t) {
     t.sp = kExactModeInit;
   }
 }
-// next record from the stack; false: the walk is over
+// next record from the stack; false: the walk is over. A return marker
+// (leaving a BLAS) sits above world entries only — instances are world
+// objects, never nested — so one pop meets at most one: straight-line code,
+// the marker's branch taken only by the lanes that leave a BLAS.
 MRT_DEV bool nf_pop(const TravIn& in, const NfStack& k, Trav& t) {
-  for (;;) {
-    if (t.sp == 0) return false;
-    t.sp -= 1;
-    t.nl = INFINITY;  // a popped node's exit is not kept (LDS: the stack's words are the walk's occupancy limit)
-    const uint32_t v = k.p[t.sp * k.stride];
-    if (v != kNfRet) {
-      t.i = v;
-      return true;
-    }
+  if (t.sp == 0) return false;
+  t.sp -= 1;
+  t.nl = INFINITY;  // a popped node's exit is not kept (LDS: the stack's words are the walk's occupancy limit)
+  uint32_t v = k.p[t.sp * k.stride];
+  if (v == kNfRet) {
     const bool inst = (t.ret & kRetInstance) != 0;
     t.ret = kNoRet;
     if (inst) {  // a model shares the world ray (and its margin)
       t.r = world_ray(in, t.ray);
       nf_margin(in, t);
     }
+    if (t.sp == 0) return false;
+    t.sp -= 1;
+    v = k.p[t.sp * k.stride];
   }
+  t.i = v;
+  return true;
 }
 MRT_DEV uint32_t vnf_entry(const DevScene& S, uint32_t base, uint32_t id, uint32_t word) {
   return S.vnf_leaf[2 * (size_t)MRT_IDX(S, S.vnf_base[base] + id, S.n_vnf, 23) + word];

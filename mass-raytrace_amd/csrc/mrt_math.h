@@ -34,6 +34,21 @@ struct V4 {
   float x, y, z, w;
 };
 
+// RN(1/x), the value `1.0f / x` has under -fhip-fp32-correctly-rounded-
+// divide-sqrt: on the device v_rcp_f32 (within an ulp) and one FMA Newton
+// step for |x| in [2^-126, 2^126) — checked equal for every one of the 2^32
+// floats (tools/rcp_check.hip) — else the IEEE division (zero, infinities,
+// NaN, subnormals, the top binade). 3 instructions instead of ~11.
+MRT_HD float rcp_cr(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float ax = fabsf(x);
+  if (ax >= 0x1p-126f && ax < 0x1p126f) {
+    const float r = __builtin_amdgcn_rcpf(x);
+    return fmaf(fmaf(-x, r, 1.0f), r, r);
+  }
+#endif
+  return 1.0f / x;
+}
 MRT_HD V2 v2(float x, float y) { return V2{x, y}; }
 MRT_HD V3 v3(float x, float y, float z) { return V3{x, y, z}; }
 MRT_HD V3 fill3(float f) { return V3{f, f, f}; }
