@@ -1006,17 +1006,13 @@ MRT_DEV void trav_box_index_nf(const TravIn& in, const NfStack& k, Trav& t, Loca
 #endif
   nf_node_test(t.s0, t.s1, t.r, in.tmin, cb, rho, h, e, x);
   const uint32_t base = t.s1.w & kNfIdx, right = base + 2u + ((t.s0.w >> 24) & 1u);  // lsz - 2 in bit 24 (layout.h)
-  if (h[0] && h[1]) {
-    const bool lfirst = !(e[1] < e[0]);
-    nf_push(k, t, lfirst ? right : base);
-    t.i = lfirst ? base : right;
-    t.nl = lfirst ? x[0] : x[1];
-  } else if (h[0] || h[1]) {
-    t.i = h[0] ? base : right;
-    t.nl = h[0] ? x[0] : x[1];
-  } else if (!nf_pop(in, k, t)) {
-    nf_over(t);
-  }
+  // selects for the next record and its exit bound, the push and the pop as
+  // the only branches (the left child when it is hit and nearer, or alone)
+  const bool left = h[0] && (!h[1] || !(e[1] < e[0]));
+  t.i = left ? base : right;
+  t.nl = left ? x[0] : x[1];
+  if (h[0] && h[1]) nf_push(k, t, left ? right : base);
+  if (!(h[0] || h[1]) && !nf_pop(in, k, t)) nf_over(t);
 }
 
 // A wild instance's leaf record (slot0.w: its WILD entry, layout.h): does the
