@@ -821,16 +821,16 @@ MRT_DEV bool nf_better(const TravIn& in, const Trav& t, float th, uint32_t prim)
   return nf_key(in, prim, t.ret) > nf_key(in, t.prim, t.hit_ret);
 }
 // a hit at th (<= the culling bound): the new best, or one of the other hits (t2)
+// (selects; the tie's key comparison, which loads, is the only branch)
 MRT_DEV void nf_hit(const TravIn& in, Trav& t, float th, uint32_t prim) {
-  if (th <= t.best && nf_better(in, t, th, prim)) {
-    t.t2 = fminf(t.t2, t.best);
-    t.best = th;
-    t.prim = prim;
-    t.hit_ret = t.ret;
-    t.nfl.rcb = nf_rho_node(t.nfl, nf_cull(th));  // a nearer bound: a smaller cap (the line stays valid below it)
-  } else {
-    t.t2 = fminf(t.t2, th);
-  }
+  bool better = th < t.best;
+  if (th == t.best) better = nf_better(in, t, th, prim);
+  t.t2 = vmin1(t.t2, better ? t.best : th);
+  t.best = better ? th : t.best;
+  t.prim = better ? prim : t.prim;
+  t.hit_ret = better ? t.ret : t.hit_ret;
+  // a nearer bound: a smaller cap (the line stays valid below it)
+  t.nfl.rcb = better ? nf_rho_node(t.nfl, nf_cull(th)) : t.nfl.rcb;
 }
 // the walk is over: k_trace checks the hit once per loop iteration (nf_finish);
 // until then the lane holds an END record, never a box (the box-run ballot)
@@ -1070,11 +1070,8 @@ MRT_DEV void trav_prim_index_nf(const TravIn& in, const NfStack& k, Trav& t, Loc
     t.i = s0.y;
     return;
   }
-  if (next != kNfPop) {
-    t.i = next;
-  } else if (!nf_pop(in, k, t)) {
-    nf_over(t);
-  }
+  t.i = next;
+  if (next == kNfPop && !nf_pop(in, k, t)) nf_over(t);
 }
 
 // Whole traversal of pool ray `ray` (one ray per thread); RNG: the
