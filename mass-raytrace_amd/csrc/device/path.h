@@ -295,6 +295,22 @@ MRT_DEV bool tri_hit(V3 a, V3 ab, V3 ac, V3 o, V3 d, float tmin, float tmax, flo
   return true;
 }
 
+// The same test without early exits (the near-first leaf step, whose lanes
+// are mixed: every lane pays the whole test either way, and the exits cost
+// exec-mask juggling): identical arithmetic, the conditions combined at the end.
+MRT_DEV bool tri_hit_nb(V3 a, V3 ab, V3 ac, V3 o, V3 d, float tmin, float tmax, float& t) {
+  V3 p_vec = cross(d, ac);
+  float det = dot(ab, p_vec);
+  float inv_det = rcp_cr(det);
+  V3 t_vec = o - a;
+  float u = dot(t_vec, p_vec) * inv_det;
+  V3 q_vec = cross(t_vec, ab);
+  float v = dot(d, q_vec) * inv_det;
+  float tt = dot(ac, q_vec) * inv_det;
+  t = tt;
+  return !(fabsf(det) < 0.000001f) && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || v + u > 1.0f) && !(tt < tmin || tt > tmax);
+}
+
 struct TriShade {
   V3 a, b, c, na, nb, nc;
   V2 uva, uvb, uvc;
@@ -1039,7 +1055,7 @@ MRT_DEV void trav_prim_index_nf(const TravIn& in, const NfStack& k, Trav& t, Loc
     V3 a{u2f(s0.x), u2f(s0.y), u2f(s0.z)}, ab{u2f(s0.w), u2f(s1.x), u2f(s1.y)}, ac{u2f(s2.x), u2f(s2.y), u2f(s2.z)};
     float th;
     // tested up to the culling bound: hits beyond `best` are recorded in t2
-    if (tri_hit(a, ab, ac, t.r.o, t.r.d, in.tmin, nf_cull(t.best), th)) {
+    if (tri_hit_nb(a, ab, ac, t.r.o, t.r.d, in.tmin, nf_cull(t.best), th)) {
       const uint32_t id = s1.z & kTriIdMask;
       if (!ALPHA || !(s1.z & kTriAlpha) || tri_alpha_pass<false, ALPHA == 2>(S, id, t.r.o, t.r.d, th, t.rng, lc))
         nf_hit(in, t, th, make_ref(MRT_REF_TRIANGLE, id));
