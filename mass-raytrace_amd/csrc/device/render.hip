@@ -340,6 +340,7 @@ struct TraceTune {
   uint32_t box_min = 24;     // inner box loop while this many lanes are at a box (65: off)
   uint32_t shade_batch = 16; // k_render: shade once this many lanes finished a segment
   uint32_t nf_batch = 32;    // near-first walk: check the hits once this many lanes' walks are over
+  uint32_t prim_run = 32;    // primitive steps alone while this many lanes are at a primitive (65: off)
 };
 
 // LDS=true: the scene's treelet (layout.h, upload.cpp build_treelet) is first
@@ -467,29 +468,42 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(NF ? (COUNT
       while (box_step() && box_step()) {
       }
       // idle lanes hold a done Trav; a near-first lane whose walk is over
-      // waits for the check below
-      const bool busy = !t[q].done && (!NF || t[q].sp != kNfDone);
-      const bool at_box = busy && trav_at_box(t[q]);
-      const unsigned long long box_mask = __ballot(at_box);
-      const unsigned long long prim_mask = __ballot(busy && !at_box);
-      // one step per busy lane (a box, or a primitive once enough lanes wait
+      // waits for the check below.
+      // One step per busy lane (a box, or a primitive once enough lanes wait
       // at one or no lane is at a box), then ONE record fetch for every lane
       // that moved: the address unit costs per wave instruction, so the box
-      // and primitive lanes share the load pair instead of issuing one each
-      const bool prim_go = (__popcll(prim_mask) >= tune.prim_batch || box_mask == 0) && busy && !at_box;
-      if (at_box) {
-        if (NF && t[q].sp != kExactMode)
-          trav_box_index_nf<COUNT>(tin, stk, t[q], lc);
-        else
-          trav_box_index<COUNT>(tin, t[q], lc);
+      // and primitive lanes share the load pair instead of issuing one each.
+      // Primitive run (the box run's mirror): while at least tune.prim_run
+      // lanes are at a primitive, they step alone (a leaf's primitives one
+      // after another) instead of paying the box branch beside each step —
+      // the same code with the box lanes masked off, so nothing is inlined twice
+      for (;;) {
+        const bool busy = !t[q].done && (!NF || t[q].sp != kNfDone);
+        const bool at_box = busy && trav_at_box(t[q]);
+        const unsigned long long box_mask = __ballot(at_box);
+        const unsigned long long prim_mask = __ballot(busy && !at_box);
+        const bool prim_run = (uint32_t)__popcll(prim_mask) >= tune.prim_run;  // wave-uniform
+        const bool box_go = at_box && !prim_run;
+        const bool prim_go = (__popcll(prim_mask) >= tune.prim_batch || box_mask == 0) && busy && !at_box;
+        if (box_go) {
+          if (NF && t[q].sp != kExactMode)
+            trav_box_index_nf<COUNT>(tin, stk, t[q], lc);
+          else
+            trav_box_index<COUNT>(tin, t[q], lc);
+        }
+        if (prim_go) {
+          if (NF && t[q].sp != kExactMode)
+            trav_prim_index_nf<COUNT, ALPHA>(tin, stk, t[q], lc);
+          else
+            trav_prim_index<COUNT, ALPHA, RNG, LDS>(tin, t[q], lc);
+        }
+        if ((box_go || prim_go) && !t[q].done && (!NF || t[q].sp != kNfDone)) trav_fetch<LDS>(tin, t[q]);
+        if (COUNT) {
+          lc.wave_slots += lane_id() == 0 ? 64u : 0u;
+          lc.lane_steps += (box_go || prim_go) ? 1u : 0u;
+        }
+        if (!prim_run) break;
       }
-      if (prim_go) {
-        if (NF && t[q].sp != kExactMode)
-          trav_prim_index_nf<COUNT, ALPHA>(tin, stk, t[q], lc);
-        else
-          trav_prim_index<COUNT, ALPHA, RNG, LDS>(tin, t[q], lc);
-      }
-      if ((at_box || prim_go) && !t[q].done && (!NF || t[q].sp != kNfDone)) trav_fetch<LDS>(tin, t[q]);
       // near-first walks that are over: check their hits (done, or the
       // reference's walk from the start) — batched: the check is a few
       // hundred wave instructions, so finished lanes wait (holding an END
@@ -503,10 +517,6 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(NF ? (COUNT
           nf_finish<COUNT>(tin, t[q], lc);
           if (!t[q].done) trav_fetch<LDS>(tin, t[q]);
         }
-      }
-      if (COUNT) {
-        lc.wave_slots += lane_id() == 0 ? 64u : 0u;
-        lc.lane_steps += (at_box || prim_go) ? 1u : 0u;
       }
     }
 #pragma unroll
@@ -1170,6 +1180,7 @@ enum OptId {
   OPT_TRACE_NF_BATCH,    // near-first walk: lanes whose walks are over wait for this many to check their hits together (-1: = refill)
   OPT_NF_KAPPA_LOG2,     // near-first walk: rays whose generic-triangle kappa exceeds 2^v take the reference walk (-8: every ray the bound covers)
   OPT_SHADE_BIN,         // k_shade: group each workgroup's survivors by material kind and direction signs (1), and split the pool by y sign (2); -1: per scene
+  OPT_TRACE_PRIM_RUN,    // k_trace: primitive run while this many lanes are at a primitive (65: off; 32: r6_s6/s7 sweeps)
   kNumOpts
 };
 struct OptDef {
@@ -1196,6 +1207,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"trace_nf_batch", -1, -1, 64},
     {"nf_kappa_log2", -8, -40, -8},
     {"shade_bin", -1, -1, 2},
+    {"trace_prim_run", 32, 1, 65},
 };
 int opt_find(const char* name) {
   if (!name) return -1;
@@ -1418,6 +1430,7 @@ void apply_options(mrt_ctx* c) {
   c->tune.chunk = o[OPT_TRACE_CHUNK] >= 0 ? (uint32_t)o[OPT_TRACE_CHUNK]
                                           : (nf ? (big_solid ? 256u : 512u) : ((big || inst) ? 128u : 512u));
   c->tune.prim_batch = (uint32_t)o[OPT_TRACE_PRIM_BATCH];
+  c->tune.prim_run = (uint32_t)o[OPT_TRACE_PRIM_RUN];
   c->tune.nf_batch = o[OPT_TRACE_NF_BATCH] > 0 ? (uint32_t)o[OPT_TRACE_NF_BATCH] : c->tune.refill;
   c->tune.shade_batch = (uint32_t)o[OPT_SHADE_BATCH];
   c->shade_wpe = o[OPT_SHADE_WAVES] >= 0 ? (int)o[OPT_SHADE_WAVES] : ((nf || big_solid) ? 7 : 8);
