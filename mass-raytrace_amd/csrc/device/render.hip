@@ -1180,7 +1180,7 @@ enum OptId {
   OPT_TRACE_NF_BATCH,    // near-first walk: lanes whose walks are over wait for this many to check their hits together (-1: = refill)
   OPT_NF_KAPPA_LOG2,     // near-first walk: rays whose generic-triangle kappa exceeds 2^v take the reference walk (-8: every ray the bound covers)
   OPT_SHADE_BIN,         // k_shade: group each workgroup's survivors by material kind and direction signs (1), and split the pool by y sign (2); -1: per scene
-  OPT_TRACE_PRIM_RUN,    // k_trace: primitive run while this many lanes are at a primitive (65: off; 32: r6_s6/s7 sweeps)
+  OPT_TRACE_PRIM_RUN,    // k_trace: primitive run while this many lanes are at a primitive (65: off; -1: 32 near-first / off)
   kNumOpts
 };
 struct OptDef {
@@ -1207,7 +1207,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"trace_nf_batch", -1, -1, 64},
     {"nf_kappa_log2", -8, -40, -8},
     {"shade_bin", -1, -1, 2},
-    {"trace_prim_run", 32, 1, 65},
+    {"trace_prim_run", -1, -1, 65},
 };
 int opt_find(const char* name) {
   if (!name) return -1;
@@ -1430,7 +1430,11 @@ void apply_options(mrt_ctx* c) {
   c->tune.chunk = o[OPT_TRACE_CHUNK] >= 0 ? (uint32_t)o[OPT_TRACE_CHUNK]
                                           : (nf ? (big_solid ? 256u : 512u) : ((big || inst) ? 128u : 512u));
   c->tune.prim_batch = (uint32_t)o[OPT_TRACE_PRIM_BATCH];
-  c->tune.prim_run = (uint32_t)o[OPT_TRACE_PRIM_RUN];
+  // primitive run (round 6, profiles/r6_primrun/): near-first walk 32
+  // (mesh_ply 1365 -> 1392, sphere_grid 1206 -> 1229, cube_field 592 -> 605);
+  // the reference walk loses with it (sphere_grid 970 -> 861, mesh_ply 1197
+  // -> 1014, cube_field 429 -> 392 in the bench line's other-walk legs): off
+  c->tune.prim_run = o[OPT_TRACE_PRIM_RUN] > 0 ? (uint32_t)o[OPT_TRACE_PRIM_RUN] : (nf ? 32u : 65u);
   c->tune.nf_batch = o[OPT_TRACE_NF_BATCH] > 0 ? (uint32_t)o[OPT_TRACE_NF_BATCH] : c->tune.refill;
   c->tune.shade_batch = (uint32_t)o[OPT_SHADE_BATCH];
   c->shade_wpe = o[OPT_SHADE_WAVES] >= 0 ? (int)o[OPT_SHADE_WAVES] : ((nf || big_solid) ? 7 : 8);
@@ -1462,6 +1466,7 @@ void set_option(mrt_ctx* c, int id, int64_t v) {
   if (id == OPT_SHADE_WAVES && v != -1 && v != 7 && v != 8)
     throw ApiError{MRT_ERR_INVALID, "option shade_waves must be 7, 8 or -1 (per scene)"};
   if (id == OPT_TRACE_NF_BATCH && v == 0) throw ApiError{MRT_ERR_INVALID, "option trace_nf_batch must be 1..64 or -1"};
+  if (id == OPT_TRACE_PRIM_RUN && v == 0) throw ApiError{MRT_ERR_INVALID, "option trace_prim_run must be 1..65 or -1"};
   if (id == OPT_TRACE_CHUNK && v != -1 && v < 64) throw ApiError{MRT_ERR_INVALID, "option trace_chunk must be >= 64 or -1"};
   if (id == OPT_QUEUES && v != c->opt[id] && c->pool_mem) {  // the pool is split per queue: reallocated at the next render
     HIP_CHECK(hipDeviceSynchronize());

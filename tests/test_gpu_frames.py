@@ -139,13 +139,14 @@ def test_shade_bin_is_bit_identical(scene, golden_dir, finish):
 @pytest.mark.parametrize("traversal", [0, 1])
 def test_prim_run_is_bit_identical(scene, golden_dir, traversal):
     """Option trace_prim_run: k_trace steps the lanes at a primitive alone
-    while at least that many are at one (65: never, 1: whenever a lane is).
+    while at least that many are at one (65: never, 1: whenever a lane is,
+    -1: the per-walk default).
     Only the order of the lanes' steps changes, never a lane's own walk, so
     the image and the work counted are the same bit for bit, on both walks."""
     for src in (scene, massrt.Builder(1).builtin("cube_field", ASPECT, golden_dir),
                 massrt.Builder(1).builtin("cornell", ASPECT, golden_dir)):
         out, cnt = [], []
-        for p in (65, 1, 32):
+        for p in (65, 1, 32, -1):
             c = massrt.Context(0, options={"trace_prim_run": p, "traversal": traversal})
             c.upload(src)
             out.append(c.render(W, H, 0, 16, seed=21))
@@ -153,7 +154,7 @@ def test_prim_run_is_bit_identical(scene, golden_dir, traversal):
             c.render(W, H, 0, 2, seed=21, counters=True)
             cnt.append(c.counters())
             c.close()
-        for j in (1, 2):
+        for j in (1, 2, 3):
             assert _same(out[0][0], out[j][0]) and _same(out[0][1], out[j][1]), j
             for k in ("samples", "segments", "bounces", "shaded", "closest_hits", "triangle_tests", "sphere_tests"):
                 assert cnt[0][k] == cnt[j][k], (j, k)
