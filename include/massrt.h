@@ -336,8 +336,8 @@ int mrt_scene_device_bytes(mrt_ctx* ctx, uint64_t* out);
  *   trace_box_min     -1, 1..65  k_trace box-run threshold (-1: per scene)
  *   trace_chunk       -1, >= 64  rays per work grab (-1: per scene)
  *   trace_prim_batch  1..64  (default 1)
- *   trace_prim_run    -1, 1..65  k_trace primitive run threshold (-1: 32 on the
- *                     near-first walk, 65 = off on the reference walk)
+ *   trace_prim_run    -1, 1..65  near-first k_trace primitive run threshold
+ *                     (-1: 32; 65: off)
  *   trace_wgs_per_cu  0..32  persistent-grid workgroups per CU (0: occupancy)
  *   shade_waves       -1, 7, 8  k_shade register budget (-1: per scene)
  *   shade_batch       1..64  fused kernel's shade batch (default 16)

@@ -482,7 +482,10 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(NF ? (COUNT
         const bool at_box = busy && trav_at_box(t[q]);
         const unsigned long long box_mask = __ballot(at_box);
         const unsigned long long prim_mask = __ballot(busy && !at_box);
-        const bool prim_run = (uint32_t)__popcll(prim_mask) >= tune.prim_run;  // wave-uniform
+        // (the near-first walk only: the reference walk's k_trace, compiled
+        // with this loop, lost 14% — 971 -> 832 on sphere_grid at any
+        // threshold, profiles/r6_primrun/ — so there it folds to one step)
+        const bool prim_run = NF && (uint32_t)__popcll(prim_mask) >= tune.prim_run;  // wave-uniform
         const bool box_go = at_box && !prim_run;
         const bool prim_go = (__popcll(prim_mask) >= tune.prim_batch || box_mask == 0) && busy && !at_box;
         if (box_go) {
@@ -1432,8 +1435,7 @@ void apply_options(mrt_ctx* c) {
   c->tune.prim_batch = (uint32_t)o[OPT_TRACE_PRIM_BATCH];
   // primitive run (round 6, profiles/r6_primrun/): near-first walk 32
   // (mesh_ply 1365 -> 1392, sphere_grid 1206 -> 1229, cube_field 592 -> 605);
-  // the reference walk loses with it (sphere_grid 970 -> 861, mesh_ply 1197
-  // -> 1014, cube_field 429 -> 392 in the bench line's other-walk legs): off
+  // the reference walk's kernel has no primitive run (k_trace)
   c->tune.prim_run = o[OPT_TRACE_PRIM_RUN] > 0 ? (uint32_t)o[OPT_TRACE_PRIM_RUN] : (nf ? 32u : 65u);
   c->tune.nf_batch = o[OPT_TRACE_NF_BATCH] > 0 ? (uint32_t)o[OPT_TRACE_NF_BATCH] : c->tune.refill;
   c->tune.shade_batch = (uint32_t)o[OPT_SHADE_BATCH];

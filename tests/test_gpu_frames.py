@@ -142,7 +142,8 @@ def test_prim_run_is_bit_identical(scene, golden_dir, traversal):
     while at least that many are at one (65: never, 1: whenever a lane is,
     -1: the per-walk default).
     Only the order of the lanes' steps changes, never a lane's own walk, so
-    the image and the work counted are the same bit for bit, on both walks."""
+    the image and the work counted are the same bit for bit (the reference
+    walk's kernel has no primitive run: the option changes nothing there)."""
     for src in (scene, massrt.Builder(1).builtin("cube_field", ASPECT, golden_dir),
                 massrt.Builder(1).builtin("cornell", ASPECT, golden_dir)):
         out, cnt = [], []
